@@ -1,0 +1,234 @@
+"""Benchmark: forward Gaussian-splat rasterization, frames/sec + Msplats/sec.
+
+Headline workload (BASELINE.json configs[2] = SURVEY.md §8(d) C3): 1M synthetic Gaussians,
+SH degree 3, 1920x1080, static camera, inputs resident in HBM.  One step = one full frame:
+preprocess (EWA + SH) -> device radix depth sort -> binning -> tile sort -> ranges -> blend,
+including the per-frame K readback the algorithm needs.  With --gpus N (one process per GPU,
+launched by torch.distributed.run) the frame's 16-px tile rows are split into N strips, every
+rank renders its strip and rank 0 gathers the frame over RCCL (strong scaling: the frame is
+fixed, N grows).
+
+Prints ONE JSON line on rank 0.  `roofline` is for the dominant kernel stage, from HIP events
+recorded on the forward's stream over the timed region; `cpu_baseline` times the CPU oracle
+(oracle/, a C port of the same forward, 1 thread) on rank 0 at N = 1.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from gaussiansplattingviewer_amd import _lib  # noqa: E402
+from gaussiansplattingviewer_amd.camera import cuda_camera_inputs, orbit_eye, static_camera  # noqa: E402
+from gaussiansplattingviewer_amd.gaussian_data import synthetic_gaussians  # noqa: E402
+from gaussiansplattingviewer_amd.rasterizer import rasterize_gaussians_native  # noqa: E402
+from gaussiansplattingviewer_amd.strips import gather_strips, strip_rows  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
+
+CONFIGS = {
+    # name: (P, W, H, sh_degree, seed, camera)
+    "c2": (100_000, 1920, 1080, 0, 1, "static"),
+    "c3": (1_000_000, 1920, 1080, 3, 2, "static"),
+    "c4": (6_000_000, 3840, 2160, 3, 3, "static"),
+    "c5": (1_000_000, 1920, 1080, 3, 2, "orbit"),
+}
+METRIC = "frames/sec + Msplats/sec, 1M Gaussians @ 1920×1080, 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="minimum CPU-oracle time to sample for cpu_baseline")
+    return ap.parse_args()
+
+
+class Scene:
+    def __init__(self, cfg, dev):
+        P, W, H, deg, seed, cam_kind = CONFIGS[cfg]
+        self.P, self.W, self.H, self.deg, self.cam_kind = P, W, H, deg, cam_kind
+        g = synthetic_gaussians(P, deg, seed)
+        self.host = g
+        up = lambda a: torch.as_tensor(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        self.xyz, self.rot, self.scale, self.opacity = up(g.xyz), up(g.rot), up(g.scale), up(g.opacity)
+        self.sh = up(g.sh).reshape(P, -1, 3).contiguous()
+        self.bg = torch.zeros(3, device=dev)
+        self.dev = dev
+        self.cams = []
+        n_cams = 1000 if cam_kind == "orbit" else 1
+        for i in range(n_cams):
+            eye = orbit_eye(i, 1000) if cam_kind == "orbit" else (0.0, 0.0, 4.0)
+            view, proj, campos, tx, ty = cuda_camera_inputs(static_camera(W, H, eye))
+            self.cams.append((up(view), up(proj), up(campos), tx, ty, (view, proj, campos)))
+
+    def render(self, step, tile_rows=None):
+        view, proj, campos, tx, ty, _ = self.cams[step % len(self.cams)]
+        return rasterize_gaussians_native(self.bg, self.xyz, None, self.opacity, self.scale,
+                                          self.rot, 1.0, None, view, proj, tx, ty, self.H, self.W,
+                                          self.sh, self.deg, campos, False, False,
+                                          tile_rows=tile_rows)
+
+
+def algorithmic_bytes(P, P_f, P_v, K, T, W, H, sh_bytes):
+    """algorithmic HBM bytes per stage of one frame."""
+    return {
+        "preprocess": 12 * P + 32 * P_f + sh_bytes * P_v + 8 * P + 40 * P_v,
+        "depth_sort": 16 * P,   # one read + write of (key, id) per Gaussian
+        "scan": 8 * P,
+        "duplicate": 4 * P + 12 * K,
+        "tile_sort": 24 * K,    # one read + write of 12-B pairs (upstream's pair size)
+        "ranges": 8 * K + 8 * T,
+        "blend": 40 * K + 12 * W * H,
+    }
+
+
+def cpu_baseline(scene, min_seconds):
+    """The oracle (C port of the forward, single thread) on a bounded sample of the same
+    workload: whole frames of the same scene and camera until min_seconds have elapsed."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # the checker's C restatement; timed here only as the CPU baseline
+    g = scene.host
+    view, proj, campos = scene.cams[0][5]
+    tx, ty = scene.cams[0][3], scene.cams[0][4]
+    frames, t0 = 0, time.perf_counter()
+    while True:
+        oracle.forward(g.xyz, g.opacity, view, proj, campos, tx, ty, scene.W, scene.H, shs=g.sh,
+                       sh_degree=scene.deg, scales=g.scale, rotations=g.rot)
+        frames += 1
+        el = time.perf_counter() - t0
+        if el >= min_seconds or frames >= 3:
+            break
+    return {"value": round(frames / el, 5), "unit": "frames/sec", "cores": 1, "kind": "port",
+            "sample": f"{frames} full frame(s) of the {scene.P}-Gaussian {scene.W}x{scene.H} "
+                      f"SH{scene.deg} scene through oracle/gsr_oracle.c (1 thread, {el:.1f} s); "
+                      f"host {platform.processor() or platform.machine()}, "
+                      f"os.cpu_count()={os.cpu_count()}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if world == 1:
+            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+
+    scene = Scene(args.config, dev)
+    W, H = scene.W, scene.H
+    gy = (H + 15) // 16
+    rows = strip_rows(gy, world, rank) if world > 1 else None
+
+    def step(i):
+        res = scene.render(i, rows)
+        if world > 1:
+            gather_strips(res.color, H, W, world, rank)
+        return res
+
+    # Warmup (also sizes the workspace so the timed loop never allocates).
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+
+    lib = _lib.load_library()
+    ctx = _lib.context(local)
+    _lib.check(lib.gsr_set_timing(ctx, 1), "gsr_set_timing")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    K_total = 0
+    for i in range(args.steps):
+        K_total += step(args.warmup + i).num_rendered
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    names = _lib.stage_names()
+    buf = (ctypes.c_float * len(names))()
+    _lib.check(lib.gsr_stage_times(ctx, buf, len(names)), "gsr_stage_times")
+    _lib.check(lib.gsr_set_timing(ctx, 0), "gsr_set_timing")
+    stage_ms = {n: float(buf[i]) for i, n in enumerate(names)}
+
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    t_max = float(t_max.item())
+
+    # Frame statistics for the algorithmic byte counts (frame 0 of the camera path, full frame).
+    res = scene.render(0, rows)
+    P = scene.P
+    P_v = int((res.radii > 0).sum().item())
+    view = scene.cams[0][0]
+    from gaussiansplattingviewer_amd.rasterizer import GaussianRasterizer, GaussianRasterizationSettings
+    P_f = int(GaussianRasterizer(GaussianRasterizationSettings(
+        H, W, 1.0, 1.0, scene.bg, 1.0, view, scene.cams[0][1], scene.deg, scene.cams[0][2],
+        False, False)).markVisible(scene.xyz).sum().item())
+    K_mean = K_total / args.steps
+    T_strip = ((rows[1] - rows[0]) if rows else gy) * ((W + 15) // 16)
+    rows_px = (min(H, rows[1] * 16) - rows[0] * 16) if rows else H
+    sh_bytes = 4 * 3 * (scene.deg + 1) ** 2
+    alg = algorithmic_bytes(P, P_f, P_v, K_mean, T_strip, W, rows_px, sh_bytes)
+    dominant = max(stage_ms, key=stage_ms.get)
+    ach = alg[dominant] / (stage_ms[dominant] * 1e-3) / 1e9
+
+    fps = args.steps / t_max
+    line = {
+        "metric": METRIC,
+        "value": round(fps, 3),
+        "unit": "frames/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * t_max / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (SURVEY.md §8(d) generator, seed %d; no PLY offline)" % CONFIGS[args.config][4],
+        "config": {"workload": f"{args.config}: {P} Gaussians, {W}x{H}, SH degree {scene.deg}, "
+                               f"{scene.cam_kind} camera",
+                   "gaussians": P, "width": W, "height": H, "sh_degree": scene.deg,
+                   "parallelism": f"image strips x{world}" + (" + RCCL gather" if world > 1 else "")},
+        "msplats_per_sec": round(P * fps / 1e6, 2),
+        "frame_stats": {"P_frustum": P_f, "P_visible": P_v, "K_pairs_mean": round(K_mean, 1),
+                        "tiles": T_strip},
+        "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
+        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "traffic": None,
+                     "bytes_per_launch": int(alg[dominant]),
+                     "frame_achieved_gbs": round(sum(alg.values()) / (1e-3 * sum(stage_ms.values())) / 1e9, 2)},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(scene, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

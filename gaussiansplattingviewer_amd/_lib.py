@@ -1,0 +1,150 @@
+"""ctypes binding of libgsr.so, the C ABI declared in include/gsr.h.
+
+This is the only way the package reaches the GPU: there is no CPU or PyTorch fallback.  If
+the library is missing or has no HIP device, every entry point raises RuntimeError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgsr.so")
+ABI_VERSION = 1
+
+GSR_OPT_BLEND_CULL = 1
+
+# Symbols include/gsr.h declares (checked by the CPU test suite).
+EXPORTED_SYMBOLS = (
+    "gsr_abi_version", "gsr_last_error", "gsr_create", "gsr_destroy", "gsr_reserve",
+    "gsr_forward", "gsr_get_binning", "gsr_mark_visible", "gsr_depth_argsort",
+    "gsr_set_timing", "gsr_stage_times", "gsr_stage_name", "gsr_set_option",
+)
+
+
+class GsrGaussians(ctypes.Structure):
+    _fields_ = [
+        ("P", ctypes.c_int64), ("D", ctypes.c_int32), ("M", ctypes.c_int32),
+        ("scale_modifier", ctypes.c_float),
+        ("means3D", ctypes.c_void_p), ("scales", ctypes.c_void_p),
+        ("rotations", ctypes.c_void_p), ("opacities", ctypes.c_void_p),
+        ("shs", ctypes.c_void_p), ("colors_precomp", ctypes.c_void_p),
+        ("cov3D_precomp", ctypes.c_void_p),
+    ]
+
+
+class GsrRasterSettings(ctypes.Structure):
+    _fields_ = [
+        ("image_width", ctypes.c_int32), ("image_height", ctypes.c_int32),
+        ("tanfovx", ctypes.c_float), ("tanfovy", ctypes.c_float),
+        ("viewmatrix", ctypes.c_void_p), ("projmatrix", ctypes.c_void_p),
+        ("campos", ctypes.c_void_p), ("bg", ctypes.c_void_p),
+        ("tile_row_begin", ctypes.c_int32), ("tile_row_end", ctypes.c_int32),
+        ("prefiltered", ctypes.c_int32), ("debug", ctypes.c_int32),
+    ]
+
+
+class GsrOutputs(ctypes.Structure):
+    _fields_ = [
+        ("color", ctypes.c_void_p), ("radii", ctypes.c_void_p),
+        ("depths", ctypes.c_void_p), ("means2D", ctypes.c_void_p),
+        ("conic_opacity", ctypes.c_void_p), ("rgb", ctypes.c_void_p),
+        ("tiles_touched", ctypes.c_void_p), ("final_T", ctypes.c_void_p),
+        ("n_contrib", ctypes.c_void_p), ("num_rendered", ctypes.c_int64),
+    ]
+
+
+_lock = threading.Lock()
+_lib = None
+_contexts: dict[int, ctypes.c_void_p] = {}
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+    lib.gsr_abi_version.restype = i32
+    lib.gsr_last_error.restype = ctypes.c_char_p
+    lib.gsr_create.argtypes = [ctypes.POINTER(vp)]
+    lib.gsr_destroy.argtypes = [vp]
+    lib.gsr_destroy.restype = None
+    lib.gsr_reserve.argtypes = [vp, i64, i64]
+    lib.gsr_forward.argtypes = [vp, ctypes.POINTER(GsrGaussians),
+                                ctypes.POINTER(GsrRasterSettings), ctypes.POINTER(GsrOutputs), vp]
+    lib.gsr_get_binning.argtypes = [vp, vp, vp, vp, ctypes.POINTER(i64),
+                                    ctypes.POINTER(ctypes.c_int32), vp]
+    lib.gsr_mark_visible.argtypes = [vp, vp, i64, vp, vp, vp, vp]
+    lib.gsr_depth_argsort.argtypes = [vp, vp, i64, ctypes.POINTER(ctypes.c_float), vp, vp, vp]
+    lib.gsr_set_timing.argtypes = [vp, i32]
+    lib.gsr_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_float), i32]
+    lib.gsr_stage_name.argtypes = [i32]
+    lib.gsr_stage_name.restype = ctypes.c_char_p
+    lib.gsr_set_option.argtypes = [vp, i32, i64]
+    for name in ("gsr_create", "gsr_reserve", "gsr_forward", "gsr_get_binning",
+                 "gsr_mark_visible", "gsr_depth_argsort", "gsr_set_timing",
+                 "gsr_stage_times", "gsr_set_option"):
+        getattr(lib, name).restype = i32
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load (once) and return libgsr.so; raise RuntimeError if it is absent or stale."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise RuntimeError(
+                f"libgsr.so not found at {path}: the HIP rasterizer is not built "
+                "(run `python -c 'import __graft_entry__ as g; g.build()'` or "
+                "`make -C gaussiansplattingviewer_amd/csrc`). There is no CPU fallback.")
+        lib = ctypes.CDLL(path)
+        _declare(lib)
+        ver = lib.gsr_abi_version()
+        if ver != ABI_VERSION:
+            raise RuntimeError(f"libgsr.so ABI version {ver} != expected {ABI_VERSION}")
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        msg = load_library().gsr_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+    return rc
+
+
+def context(device_index: int) -> ctypes.c_void_p:
+    """The process-wide gsr_context of a device (created on first use, on that device)."""
+    import torch
+
+    lib = load_library()
+    with _lock:
+        ctx = _contexts.get(device_index)
+        if ctx is not None:
+            return ctx
+        if not torch.cuda.is_available():
+            raise RuntimeError("gaussiansplattingviewer_amd needs a HIP device (MI355X); "
+                               "torch.cuda.is_available() is False")
+        with torch.cuda.device(device_index):
+            ctx = ctypes.c_void_p()
+            check(lib.gsr_create(ctypes.byref(ctx)), "gsr_create")
+        _contexts[device_index] = ctx
+        return ctx
+
+
+def stage_names() -> list[str]:
+    lib = load_library()
+    names = []
+    i = 0
+    while True:
+        n = lib.gsr_stage_name(i).decode()
+        if not n:
+            return names
+        names.append(n)
+        i += 1
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None for an absent / empty optional tensor)."""
+    if t is None or t.numel() == 0:
+        return None
+    return t.data_ptr()

@@ -1,0 +1,483 @@
+// api.hip -- the C ABI of libgsr.so (declared in include/gsr.h): workspace ownership,
+// argument validation, stage orchestration on the caller's stream, stage timing.
+//
+// gsr_forward replaces upstream `_C.rasterize_gaussians` / Rasterizer::forward
+// (rasterizer_impl.cu), which the viewer reaches through renderer_cuda.py:211-224.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "gsr.h"
+#include "gsr_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define GSR_HIP(call, what)                                                                  \
+    do {                                                                                     \
+        hipError_t e_ = (call);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail(GSR_E_HIP, std::string(what) + ": " + hipGetErrorString(e_));        \
+    } while (0)
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+};
+
+constexpr int kStages = 7;
+constexpr int kTimingRing = 256;  // frames whose stage events are kept
+const char *kStageNames[kStages] = {"preprocess", "depth_sort", "scan",  "duplicate",
+                                    "tile_sort",  "ranges",     "blend"};
+
+}  // namespace
+
+struct gsr_context {
+    int device = 0;
+    // per-Gaussian workspace
+    DevBuf records, strip_tiles, sort_keys, sort_vals, sort_keys_alt, sort_vals_alt, partials,
+        total, hist, digit_total;
+    // per-pair workspace
+    DevBuf tile_keys, tile_vals, tile_keys_alt, tile_vals_alt;
+    DevBuf ranges_local;
+    uint64_t *h_total = nullptr;  // pinned
+    // state of the last forward (for gsr_get_binning)
+    bool have_forward = false;
+    int64_t last_K = 0;
+    uint32_t last_gx = 0, last_gy = 0, last_rb = 0, last_re = 0;
+    uint32_t *last_point_list = nullptr, *last_tiles_local = nullptr;
+    // options / timing
+    int cull = 1;
+    // Stage timing: a ring of event sets, one per forward, read back after the timed region.
+    bool timing = false;
+    int64_t timed_frames = 0;
+    hipEvent_t ev[kTimingRing][kStages + 1] = {};
+};
+
+namespace {
+
+// Grow-only device buffer.  The stream is drained first so no in-flight kernel still reads
+// the old allocation.
+int grow(gsr_context *ctx, DevBuf &b, size_t bytes, hipStream_t s) {
+    if (bytes <= b.cap) return GSR_OK;
+    size_t want = std::max(bytes, b.cap + b.cap / 2);
+    want = (want + 255) & ~size_t(255);
+    if (b.p) {
+        GSR_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(grow)");
+        GSR_HIP(hipFree(b.p), "hipFree");
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    if (hipMalloc(&b.p, want) != hipSuccess) {
+        (void)hipGetLastError();
+        b.p = nullptr;
+        return fail(GSR_E_NOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
+    }
+    b.cap = want;
+    (void)ctx;
+    return GSR_OK;
+}
+
+#define GSR_TRY(expr)                 \
+    do {                              \
+        int rc_ = (expr);             \
+        if (rc_ != GSR_OK) return rc_; \
+    } while (0)
+
+int reserve_P(gsr_context *ctx, int64_t P, hipStream_t s) {
+    const size_t n = (size_t)std::max<int64_t>(P, 1);
+    GSR_TRY(grow(ctx, ctx->records, n * sizeof(gsr::SplatRecord), s));
+    GSR_TRY(grow(ctx, ctx->strip_tiles, n * 4, s));
+    GSR_TRY(grow(ctx, ctx->sort_keys, n * 4, s));
+    GSR_TRY(grow(ctx, ctx->sort_vals, n * 4, s));
+    GSR_TRY(grow(ctx, ctx->sort_keys_alt, n * 4, s));
+    GSR_TRY(grow(ctx, ctx->sort_vals_alt, n * 4, s));
+    GSR_TRY(grow(ctx, ctx->partials, (size_t)std::max<int64_t>(gsr_scan_blocks(P), 1) * 4, s));
+    GSR_TRY(grow(ctx, ctx->total, 16, s));
+    GSR_TRY(grow(ctx, ctx->hist, (size_t)gsr_radix_hist_words(P) * 4, s));
+    GSR_TRY(grow(ctx, ctx->digit_total, 256 * 4, s));
+    return GSR_OK;
+}
+
+int reserve_K(gsr_context *ctx, int64_t K, hipStream_t s) {
+    const size_t n = (size_t)std::max<int64_t>(K, 1);
+    GSR_TRY(grow(ctx, ctx->tile_keys, n * 4, s));
+    GSR_TRY(grow(ctx, ctx->tile_vals, n * 4, s));
+    GSR_TRY(grow(ctx, ctx->tile_keys_alt, n * 4, s));
+    GSR_TRY(grow(ctx, ctx->tile_vals_alt, n * 4, s));
+    GSR_TRY(grow(ctx, ctx->hist, (size_t)gsr_radix_hist_words(K) * 4, s));
+    return GSR_OK;
+}
+
+int bits_for(uint64_t max_value) {  // bits needed to represent every value <= max_value
+    int b = 0;
+    while (b < 32 && (max_value >> b) != 0) ++b;
+    return b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gsr_abi_version(void) { return GSR_ABI_VERSION; }
+const char *gsr_last_error(void) { return g_err.c_str(); }
+const char *gsr_stage_name(int i) { return (i >= 0 && i < kStages) ? kStageNames[i] : ""; }
+
+int gsr_create(gsr_context **out) {
+    if (!out) return fail(GSR_E_INVALID, "gsr_create: out is NULL");
+    *out = nullptr;
+    gsr_context *ctx = new gsr_context();
+    if (hipGetDevice(&ctx->device) != hipSuccess) {
+        (void)hipGetLastError();
+        delete ctx;
+        return fail(GSR_E_HIP, "gsr_create: no HIP device");
+    }
+    if (hipHostMalloc(reinterpret_cast<void **>(&ctx->h_total), sizeof(uint64_t)) != hipSuccess) {
+        (void)hipGetLastError();
+        delete ctx;
+        return fail(GSR_E_HIP, "gsr_create: hipHostMalloc failed");
+    }
+    for (auto &set : ctx->ev)
+        for (auto &e : set) {
+            if (hipEventCreate(&e) != hipSuccess) {
+                (void)hipGetLastError();
+                gsr_destroy(ctx);
+                return fail(GSR_E_HIP, "gsr_create: hipEventCreate failed");
+            }
+        }
+    *out = ctx;
+    return GSR_OK;
+}
+
+void gsr_destroy(gsr_context *ctx) {
+    if (!ctx) return;
+    (void)hipDeviceSynchronize();
+    DevBuf *bufs[] = {&ctx->records,       &ctx->strip_tiles,   &ctx->sort_keys,
+                      &ctx->sort_vals,     &ctx->sort_keys_alt, &ctx->sort_vals_alt,
+                      &ctx->partials,      &ctx->total,         &ctx->hist,
+                      &ctx->digit_total,   &ctx->tile_keys,     &ctx->tile_vals,
+                      &ctx->tile_keys_alt, &ctx->tile_vals_alt, &ctx->ranges_local};
+    for (DevBuf *b : bufs)
+        if (b->p) (void)hipFree(b->p);
+    for (auto &set : ctx->ev)
+        for (auto &e : set)
+            if (e) (void)hipEventDestroy(e);
+    if (ctx->h_total) (void)hipHostFree(ctx->h_total);
+    delete ctx;
+}
+
+int gsr_reserve(gsr_context *ctx, int64_t P, int64_t K) {
+    if (!ctx || P < 0 || K < 0) return fail(GSR_E_INVALID, "gsr_reserve: bad arguments");
+    GSR_TRY(reserve_P(ctx, P, nullptr));
+    GSR_TRY(reserve_K(ctx, K, nullptr));
+    GSR_HIP(hipDeviceSynchronize(), "gsr_reserve");
+    return GSR_OK;
+}
+
+int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
+    if (!ctx) return fail(GSR_E_INVALID, "gsr_set_option: NULL context");
+    if (option == GSR_OPT_BLEND_CULL) {
+        ctx->cull = value ? 1 : 0;
+        return GSR_OK;
+    }
+    return fail(GSR_E_INVALID, "gsr_set_option: unknown option " + std::to_string(option));
+}
+
+int gsr_set_timing(gsr_context *ctx, int enable) {
+    if (!ctx) return fail(GSR_E_INVALID, "gsr_set_timing: NULL context");
+    ctx->timing = enable != 0;
+    ctx->timed_frames = 0;
+    return GSR_OK;
+}
+
+// Mean per-stage time (ms) over the timed forwards since gsr_set_timing(1) (the most recent
+// kTimingRing of them).  Waits for the last one; returns the number of frames averaged in
+// *n_frames if non-NULL.  Return value: number of stages.
+int gsr_stage_times(gsr_context *ctx, float *ms, int n) {
+    if (!ctx || (!ms && n > 0)) return fail(GSR_E_INVALID, "gsr_stage_times: bad arguments");
+    if (ctx->timed_frames == 0) return fail(GSR_E_STATE, "gsr_stage_times: no timed forward yet");
+    const int64_t frames = std::min<int64_t>(ctx->timed_frames, kTimingRing);
+    const int64_t last = (ctx->timed_frames - 1) % kTimingRing;
+    GSR_HIP(hipEventSynchronize(ctx->ev[last][kStages]), "hipEventSynchronize");
+    double acc[kStages] = {};
+    for (int64_t f = 0; f < frames; ++f) {
+        const int64_t slot = (ctx->timed_frames - 1 - f) % kTimingRing;
+        for (int i = 0; i < kStages; ++i) {
+            float t = 0.f;
+            GSR_HIP(hipEventElapsedTime(&t, ctx->ev[slot][i], ctx->ev[slot][i + 1]),
+                    "hipEventElapsedTime");
+            acc[i] += t;
+        }
+    }
+    for (int i = 0; i < kStages && i < n; ++i) ms[i] = (float)(acc[i] / (double)frames);
+    return kStages;
+}
+
+int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings *st,
+                gsr_outputs *out, void *stream_) {
+    if (!ctx || !g || !st || !out) return fail(GSR_E_INVALID, "gsr_forward: NULL argument");
+    hipStream_t s = static_cast<hipStream_t>(stream_);
+    const int64_t P = g->P;
+    const int W = st->image_width, H = st->image_height;
+    if (P < 0 || P > (int64_t)UINT32_MAX) return fail(GSR_E_INVALID, "gsr_forward: bad P");
+    if (W <= 0 || H <= 0) return fail(GSR_E_INVALID, "gsr_forward: image size must be positive");
+    if (!out->color || (P > 0 && !out->radii))
+        return fail(GSR_E_INVALID, "gsr_forward: color and radii outputs are required");
+    if (P > 0) {
+        if (!g->means3D || !g->opacities)
+            return fail(GSR_E_INVALID, "gsr_forward: means3D and opacities are required");
+        if ((g->shs == nullptr) == (g->colors_precomp == nullptr))
+            return fail(GSR_E_INVALID,
+                        "Please provide excatly one of either SHs or precomputed colors!");
+        if (((g->scales == nullptr || g->rotations == nullptr) && g->cov3D_precomp == nullptr) ||
+            ((g->scales != nullptr || g->rotations != nullptr) && g->cov3D_precomp != nullptr))
+            return fail(GSR_E_INVALID, "Please provide exactly one of either scale/rotation pair "
+                                       "or precomputed 3D covariance!");
+        if (g->shs && (g->M <= 0 || g->D < 0 || g->D > 3 || (g->D + 1) * (g->D + 1) > g->M))
+            return fail(GSR_E_INVALID, "gsr_forward: sh_degree " + std::to_string(g->D) +
+                                           " needs (deg+1)^2 <= " + std::to_string(g->M) +
+                                           " stored coefficients (deg <= 3)");
+        if (!st->viewmatrix || !st->projmatrix || (g->shs && !st->campos))
+            return fail(GSR_E_INVALID, "gsr_forward: camera matrices are required");
+    }
+    if (!st->bg) return fail(GSR_E_INVALID, "gsr_forward: bg is required");
+
+    const uint32_t gx = (uint32_t)((W + GSR_TILE_X - 1) / GSR_TILE_X);
+    const uint32_t gy = (uint32_t)((H + GSR_TILE_Y - 1) / GSR_TILE_Y);
+    uint32_t rb = 0, re = gy;
+    if (st->tile_row_begin != 0 || st->tile_row_end != 0) {
+        if (st->tile_row_begin < 0 || st->tile_row_end > (int)gy ||
+            st->tile_row_begin >= st->tile_row_end)
+            return fail(GSR_E_INVALID, "gsr_forward: bad tile row strip");
+        rb = (uint32_t)st->tile_row_begin;
+        re = (uint32_t)st->tile_row_end;
+    }
+    const uint32_t rows_tiles = re - rb;
+    const int y0 = (int)(rb * GSR_TILE_Y);
+    const int rows_out = std::min(H, (int)(re * GSR_TILE_Y)) - y0;
+    const uint64_t T_strip = (uint64_t)gx * rows_tiles;
+
+    ctx->have_forward = false;
+    const bool dbg = st->debug != 0;
+    hipEvent_t *ev = ctx->ev[ctx->timed_frames % kTimingRing];
+    auto stage_end = [&](int i) -> int {
+        if (ctx->timing) GSR_HIP(hipEventRecord(ev[i + 1], s), "hipEventRecord");
+        if (dbg) {
+            GSR_HIP(hipStreamSynchronize(s), std::string("stage ") + kStageNames[i]);
+            GSR_HIP(hipGetLastError(), std::string("stage ") + kStageNames[i]);
+        }
+        return GSR_OK;
+    };
+
+    GSR_TRY(reserve_P(ctx, P, s));
+    GSR_TRY(grow(ctx, ctx->ranges_local, (size_t)std::max<uint64_t>(T_strip, 1) * 8, s));
+
+    if (P == 0) {  // upstream returns the zero-initialised image without rendering
+        GSR_HIP(hipMemsetAsync(out->color, 0, (size_t)3 * rows_out * W * sizeof(float), s),
+                "hipMemsetAsync(color)");
+        GSR_HIP(hipMemsetAsync(ctx->ranges_local.p, 0, T_strip * 8, s), "hipMemsetAsync");
+        out->num_rendered = 0;
+        ctx->last_K = 0;
+        ctx->last_gx = gx; ctx->last_gy = gy; ctx->last_rb = rb; ctx->last_re = re;
+        ctx->last_point_list = static_cast<uint32_t *>(ctx->tile_vals.p);
+        ctx->last_tiles_local = static_cast<uint32_t *>(ctx->tile_keys.p);
+        ctx->have_forward = true;
+        return GSR_OK;
+    }
+
+    if (ctx->timing) GSR_HIP(hipEventRecord(ev[0], s), "hipEventRecord");
+
+    // ---- 1. preprocess -------------------------------------------------------------------
+    GsrPreprocessArgs pa{};
+    pa.P = P;
+    pa.D = g->D;
+    pa.M = g->M;
+    pa.scale_modifier = g->scale_modifier;
+    pa.means3D = g->means3D;
+    pa.scales = g->scales;
+    pa.rotations = g->rotations;
+    pa.opacities = g->opacities;
+    pa.shs = g->shs;
+    pa.colors_precomp = g->colors_precomp;
+    pa.cov3D_precomp = g->cov3D_precomp;
+    pa.viewmatrix = st->viewmatrix;
+    pa.projmatrix = st->projmatrix;
+    pa.campos = st->campos;
+    pa.tanfovx = st->tanfovx;
+    pa.tanfovy = st->tanfovy;
+    // rasterizer_impl.cu: focal_y = height / (2.0f * tan_fovy); focal_x likewise (float).
+    pa.focal_y = (float)H / (2.0f * st->tanfovy);
+    pa.focal_x = (float)W / (2.0f * st->tanfovx);
+    pa.W = W;
+    pa.H = H;
+    pa.grid_x = gx;
+    pa.grid_y = gy;
+    pa.row_begin = rb;
+    pa.row_end = re;
+    pa.prefiltered = st->prefiltered;
+    pa.sh_vec4 = (g->shs && g->M == 16 && (reinterpret_cast<uintptr_t>(g->shs) & 15) == 0) ? 1 : 0;
+    pa.rot_vec4 = (g->rotations && (reinterpret_cast<uintptr_t>(g->rotations) & 15) == 0) ? 1 : 0;
+    pa.radii = out->radii;
+    pa.records = static_cast<gsr::SplatRecord *>(ctx->records.p);
+    pa.sort_keys = static_cast<uint32_t *>(ctx->sort_keys.p);
+    pa.sort_vals = static_cast<uint32_t *>(ctx->sort_vals.p);
+    pa.strip_tiles = static_cast<uint32_t *>(ctx->strip_tiles.p);
+    pa.depths = out->depths;
+    pa.means2D = out->means2D;
+    pa.conic_opacity = out->conic_opacity;
+    pa.rgb = out->rgb;
+    pa.tiles_touched = out->tiles_touched;
+    if (pa.conic_opacity && (reinterpret_cast<uintptr_t>(pa.conic_opacity) & 15) != 0)
+        return fail(GSR_E_INVALID, "gsr_forward: conic_opacity output must be 16-B aligned");
+    GSR_HIP(gsr_launch_preprocess(pa, s), "preprocess launch");
+    GSR_TRY(stage_end(0));
+
+    // ---- 2. stable radix sort of the Gaussians by view depth ------------------------------
+    uint32_t *dk = pa.sort_keys, *dv = pa.sort_vals;
+    uint32_t *dk_alt = static_cast<uint32_t *>(ctx->sort_keys_alt.p);
+    uint32_t *dv_alt = static_cast<uint32_t *>(ctx->sort_vals_alt.p);
+    uint32_t *hist = static_cast<uint32_t *>(ctx->hist.p);
+    uint32_t *digit_total = static_cast<uint32_t *>(ctx->digit_total.p);
+    GSR_HIP(gsr_radix_sort_pairs(&dk, &dv, &dk_alt, &dv_alt, P, 0, 32, hist, digit_total, s),
+            "depth sort launch");
+    GSR_TRY(stage_end(1));
+    const uint32_t *perm = dv;
+
+    // ---- 3. offsets scan over depth-sorted strip tile counts; K readback --------------------
+    uint32_t *partials = static_cast<uint32_t *>(ctx->partials.p);
+    uint64_t *d_total = static_cast<uint64_t *>(ctx->total.p);
+    GSR_HIP(gsr_launch_scan_reduce(perm, pa.strip_tiles, P, partials, s), "scan launch");
+    GSR_HIP(gsr_launch_scan_partials(partials, gsr_scan_blocks(P), d_total, s), "scan launch");
+    GSR_HIP(hipMemcpyAsync(ctx->h_total, d_total, sizeof(uint64_t), hipMemcpyDeviceToHost, s),
+            "hipMemcpyAsync(num_rendered)");
+    GSR_TRY(stage_end(2));
+    GSR_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(num_rendered)");
+    const uint64_t K = *ctx->h_total;
+    if (K > (uint64_t)UINT32_MAX)
+        return fail(GSR_E_INVALID, "gsr_forward: more than 2^32-1 (Gaussian, tile) pairs");
+    GSR_TRY(reserve_K(ctx, (int64_t)K, s));
+
+    // ---- 4. duplicate into (tile, Gaussian) pairs, depth order -------------------------------
+    uint32_t *tk = static_cast<uint32_t *>(ctx->tile_keys.p);
+    uint32_t *tv = static_cast<uint32_t *>(ctx->tile_vals.p);
+    uint32_t *tk_alt = static_cast<uint32_t *>(ctx->tile_keys_alt.p);
+    uint32_t *tv_alt = static_cast<uint32_t *>(ctx->tile_vals_alt.p);
+    hist = static_cast<uint32_t *>(ctx->hist.p);  // may have been regrown
+    GSR_HIP(gsr_launch_duplicate(perm, pa.strip_tiles, partials, P, pa.records, gx, gy, rb, re, tk,
+                                 tv, s),
+            "duplicate launch");
+    GSR_TRY(stage_end(3));
+
+    // ---- 5. stable radix sort of the pairs by (strip-local) tile id -------------------------
+    const int tbits = T_strip > 1 ? bits_for(T_strip - 1) : 0;
+    GSR_HIP(gsr_radix_sort_pairs(&tk, &tv, &tk_alt, &tv_alt, (int64_t)K, 0, tbits, hist,
+                                 digit_total, s),
+            "tile sort launch");
+    GSR_TRY(stage_end(4));
+
+    // ---- 6. tile ranges ----------------------------------------------------------------------
+    GSR_HIP(hipMemsetAsync(ctx->ranges_local.p, 0, T_strip * 8, s), "hipMemsetAsync(ranges)");
+    GSR_HIP(gsr_launch_ranges(tk, (int64_t)K, static_cast<uint32_t *>(ctx->ranges_local.p), s),
+            "ranges launch");
+    GSR_TRY(stage_end(5));
+
+    // ---- 7. blend ------------------------------------------------------------------------------
+    GsrBlendArgs ba{};
+    ba.ranges = static_cast<const uint2 *>(ctx->ranges_local.p);
+    ba.point_list = tv;
+    ba.records = pa.records;
+    ba.W = W;
+    ba.H = H;
+    ba.grid_x = gx;
+    ba.row_begin = rb;
+    ba.rows_tiles = rows_tiles;
+    ba.y0 = y0;
+    ba.rows_out = rows_out;
+    ba.bg = st->bg;
+    ba.out_color = out->color;
+    ba.final_T = out->final_T;
+    ba.n_contrib = out->n_contrib;
+    ba.cull = ctx->cull;
+    GSR_HIP(gsr_launch_blend(ba, s), "blend launch");
+    GSR_TRY(stage_end(6));
+
+    out->num_rendered = (int64_t)K;
+    ctx->last_K = (int64_t)K;
+    ctx->last_gx = gx; ctx->last_gy = gy; ctx->last_rb = rb; ctx->last_re = re;
+    ctx->last_point_list = tv;
+    ctx->last_tiles_local = tk;
+
+    ctx->have_forward = true;
+    if (ctx->timing) ++ctx->timed_frames;
+    return GSR_OK;
+}
+
+int gsr_get_binning(gsr_context *ctx, uint32_t *point_list, uint32_t *point_tiles,
+                    uint32_t *ranges, int64_t *num_rendered, int32_t *num_tiles, void *stream) {
+    if (!ctx) return fail(GSR_E_INVALID, "gsr_get_binning: NULL context");
+    if (!ctx->have_forward) return fail(GSR_E_STATE, "gsr_get_binning: no forward yet");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t K = ctx->last_K;
+    const uint64_t T = (uint64_t)ctx->last_gx * ctx->last_gy;
+    const uint64_t off = (uint64_t)ctx->last_rb * ctx->last_gx;
+    const uint64_t T_strip = (uint64_t)ctx->last_gx * (ctx->last_re - ctx->last_rb);
+    if (num_rendered) *num_rendered = K;
+    if (num_tiles) *num_tiles = (int32_t)T;
+    if (point_list && K > 0)
+        GSR_HIP(hipMemcpyAsync(point_list, ctx->last_point_list, (size_t)K * 4,
+                               hipMemcpyDeviceToDevice, s),
+                "hipMemcpyAsync(point_list)");
+    if (point_tiles)
+        GSR_HIP(gsr_launch_globalize_tiles(ctx->last_tiles_local, K, (uint32_t)off, point_tiles, s),
+                "globalize launch");
+    if (ranges) {
+        GSR_HIP(hipMemsetAsync(ranges, 0, T * 8, s), "hipMemsetAsync(ranges)");
+        GSR_HIP(hipMemcpyAsync(reinterpret_cast<char *>(ranges) + off * 8, ctx->ranges_local.p,
+                               T_strip * 8, hipMemcpyDeviceToDevice, s),
+                "hipMemcpyAsync(ranges)");
+    }
+    GSR_HIP(hipStreamSynchronize(s), "gsr_get_binning");
+    return GSR_OK;
+}
+
+int gsr_mark_visible(gsr_context *ctx, const float *means3D, int64_t P, const float *viewmatrix,
+                     const float *projmatrix, uint8_t *visible, void *stream) {
+    (void)projmatrix;  // upstream in_frustum only tests view-space depth
+    if (!ctx || P < 0 || (P > 0 && (!means3D || !viewmatrix || !visible)))
+        return fail(GSR_E_INVALID, "gsr_mark_visible: bad arguments");
+    GSR_HIP(gsr_launch_mark_visible(means3D, P, viewmatrix, visible,
+                                    static_cast<hipStream_t>(stream)),
+            "mark_visible launch");
+    return GSR_OK;
+}
+
+int gsr_depth_argsort(gsr_context *ctx, const float *xyz, int64_t P, const float *view_host16,
+                      int32_t *out_index, float *out_depth, void *stream) {
+    if (!ctx || P < 0 || !view_host16 || (P > 0 && (!xyz || !out_index)))
+        return fail(GSR_E_INVALID, "gsr_depth_argsort: bad arguments");
+    if (P > (int64_t)INT32_MAX) return fail(GSR_E_INVALID, "gsr_depth_argsort: P too large");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (P == 0) return GSR_OK;
+    GSR_TRY(reserve_P(ctx, P, s));
+    uint32_t *k = static_cast<uint32_t *>(ctx->sort_keys.p);
+    uint32_t *v = static_cast<uint32_t *>(ctx->sort_vals.p);
+    uint32_t *ka = static_cast<uint32_t *>(ctx->sort_keys_alt.p);
+    uint32_t *va = static_cast<uint32_t *>(ctx->sort_vals_alt.p);
+    GSR_HIP(gsr_launch_view_depth_keys(xyz, P, view_host16[8], view_host16[9], view_host16[10],
+                                       view_host16[11], k, v, out_depth, s),
+            "view depth launch");
+    GSR_HIP(gsr_radix_sort_pairs(&k, &v, &ka, &va, P, 0, 32, static_cast<uint32_t *>(ctx->hist.p),
+                                 static_cast<uint32_t *>(ctx->digit_total.p), s),
+            "depth argsort launch");
+    GSR_HIP(gsr_launch_index_to_i32(v, P, out_index, s), "index launch");
+    return GSR_OK;
+}
+
+}  // extern "C"

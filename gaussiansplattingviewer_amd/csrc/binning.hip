@@ -1,0 +1,164 @@
+// binning.hip -- tile binning for gfx950: offsets scan, pair duplication, tile ranges.
+//
+// Replaces upstream rasterizer_impl.cu  cub::DeviceScan::InclusiveSum(tiles_touched) +
+// duplicateWithKeys + identifyTileRanges.  The design difference (documented in DESIGN.md):
+// upstream builds 64-bit (tile << 32 | depth) keys in Gaussian-index order and radix-sorts
+// K of them over 32 + log2(T) bits.  Here the Gaussians are first sorted by depth (P keys,
+// stable), the pairs are emitted in that order, and a stable sort on the tile id alone
+// (log2(T) bits) finishes the job.  Within a tile the result is ordered by depth and then
+// by Gaussian index, exactly as upstream's stable 64-bit sort orders it, so point lists and
+// ranges are bit-identical while the K-sized sort moves 8-B pairs over 2 passes instead of
+// 12-B pairs over 6.
+#include "gsr_internal.h"
+
+using namespace gsr;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kItems = 16;
+constexpr int kTile = kBlock * kItems;  // 4096 depth-sorted Gaussians per block
+
+// Pass 1 of the scan: per-block sum of the strip tile counts, gathered in depth order.
+__global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t *__restrict__ perm,
+                                                        const uint32_t *__restrict__ strip_tiles,
+                                                        int64_t n, uint32_t *__restrict__ partials) {
+    __shared__ uint32_t s_tmp[4];
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    uint32_t sum = 0;
+#pragma unroll 4
+    for (int j = 0; j < kItems; ++j) {
+        const int64_t e = base + j * kBlock + threadIdx.x;
+        if (e < n) sum += strip_tiles[perm[e]];
+    }
+    uint32_t total;
+    block256_exclusive_scan(sum, s_tmp, total);
+    if (threadIdx.x == 0) partials[blockIdx.x] = total;
+}
+
+// Pass 2: single block, exclusive scan of the block partials; K -> *total (64-bit, so an
+// overflow of the 32-bit pair index is detected on the host).
+__global__ __launch_bounds__(kBlock) void k_scan_partials(uint32_t *__restrict__ partials,
+                                                          int64_t nb, uint64_t *__restrict__ total) {
+    __shared__ uint32_t s_tmp[4];
+    uint64_t carry = 0;
+    for (int64_t start = 0; start < nb; start += kBlock) {
+        const int64_t e = start + threadIdx.x;
+        const uint32_t v = e < nb ? partials[e] : 0u;
+        uint32_t t;
+        const uint32_t pre = block256_exclusive_scan(v, s_tmp, t);
+        if (e < nb) partials[e] = (uint32_t)(carry + pre);
+        carry += t;
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+// Pass 3 fused with upstream duplicateWithKeys: block scan of the tile counts of 4096
+// depth-sorted Gaussians (blocked: thread t owns elements 16t..16t+15), then every Gaussian
+// writes one (strip-local tile id, Gaussian id) pair per tile of its rect inside the strip,
+// row-major like upstream.
+__global__ __launch_bounds__(kBlock) void k_duplicate(
+    const uint32_t *__restrict__ perm, const uint32_t *__restrict__ strip_tiles,
+    const uint32_t *__restrict__ partials, int64_t n, const SplatRecord *__restrict__ records,
+    uint32_t gx, uint32_t gy, uint32_t row_begin, uint32_t row_end, uint32_t *__restrict__ tile_keys,
+    uint32_t *__restrict__ tile_vals) {
+    __shared__ uint32_t s_tmp[4];
+    const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kItems;
+    uint32_t id[kItems], cnt[kItems], sum = 0;
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+        const int64_t e = base + j;
+        id[j] = e < n ? perm[e] : 0u;
+        cnt[j] = e < n ? strip_tiles[id[j]] : 0u;
+        sum += cnt[j];
+    }
+    uint32_t total;
+    uint32_t off = block256_exclusive_scan(sum, s_tmp, total) + partials[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+        if (cnt[j] == 0) continue;
+        const SplatRecord &r = records[id[j]];
+        const float4 a = r.a;
+        const int radius = __float_as_int(r.c.w);
+        const Rect rc = get_rect(a.x, a.y, radius, gx, gy);
+        const uint32_t y0 = max(rc.y0, row_begin), y1 = min(rc.y1, row_end);
+        for (uint32_t y = y0; y < y1; ++y) {
+            const uint32_t row = (y - row_begin) * gx;
+            for (uint32_t x = rc.x0; x < rc.x1; ++x) {
+                tile_keys[off] = row + x;
+                tile_vals[off] = id[j];
+                ++off;
+            }
+        }
+    }
+}
+
+// upstream identifyTileRanges over the tile-sorted keys (ranges pre-zeroed).
+__global__ __launch_bounds__(kBlock) void k_ranges(const uint32_t *__restrict__ tile_keys,
+                                                   int64_t K, uint32_t *__restrict__ ranges) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= K) return;
+    const uint32_t cur = tile_keys[i];
+    if (i == 0) {
+        ranges[2 * cur] = 0;
+    } else {
+        const uint32_t prev = tile_keys[i - 1];
+        if (cur != prev) {
+            ranges[2 * prev + 1] = (uint32_t)i;
+            ranges[2 * cur] = (uint32_t)i;
+        }
+    }
+    if (i == K - 1) ranges[2 * cur + 1] = (uint32_t)K;
+}
+
+__global__ __launch_bounds__(kBlock) void k_globalize(const uint32_t *__restrict__ local, int64_t K,
+                                                      uint32_t offset, uint32_t *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < K) out[i] = local[i] + offset;
+}
+
+}  // namespace
+
+int64_t gsr_scan_blocks(int64_t n) { return (n + kTile - 1) / kTile; }
+
+hipError_t gsr_launch_scan_reduce(const uint32_t *perm, const uint32_t *strip_tiles, int64_t n,
+                                  uint32_t *partials, hipStream_t s) {
+    const int64_t nb = gsr_scan_blocks(n);
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(kBlock), 0, s, perm, strip_tiles, n,
+                       partials);
+    return hipGetLastError();
+}
+
+hipError_t gsr_launch_scan_partials(uint32_t *partials, int64_t nb, uint64_t *total,
+                                    hipStream_t s) {
+    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kBlock), 0, s, partials, nb, total);
+    return hipGetLastError();
+}
+
+hipError_t gsr_launch_duplicate(const uint32_t *perm, const uint32_t *strip_tiles,
+                                const uint32_t *partials, int64_t n, const SplatRecord *records,
+                                uint32_t gx, uint32_t gy, uint32_t row_begin, uint32_t row_end,
+                                uint32_t *tile_keys, uint32_t *tile_vals, hipStream_t s) {
+    const int64_t nb = gsr_scan_blocks(n);
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_duplicate, dim3((unsigned)nb), dim3(kBlock), 0, s, perm, strip_tiles,
+                       partials, n, records, gx, gy, row_begin, row_end, tile_keys, tile_vals);
+    return hipGetLastError();
+}
+
+hipError_t gsr_launch_ranges(const uint32_t *tile_keys, int64_t K, uint32_t *ranges,
+                             hipStream_t s) {
+    if (K == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ranges, dim3((unsigned)((K + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                       tile_keys, K, ranges);
+    return hipGetLastError();
+}
+
+hipError_t gsr_launch_globalize_tiles(const uint32_t *local, int64_t K, uint32_t offset,
+                                      uint32_t *global, hipStream_t s) {
+    if (K == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_globalize, dim3((unsigned)((K + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       s, local, K, offset, global);
+    return hipGetLastError();
+}

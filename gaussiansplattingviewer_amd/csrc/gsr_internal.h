@@ -1,0 +1,262 @@
+// gsr_internal.h -- device-side building blocks shared by the gsr kernels (gfx950 only).
+//
+// Arithmetic contract: every float expression below is evaluated in exactly the order the
+// upstream diff-gaussian-rasterization C++ writes it (left-to-right sums, glm column-major
+// mat3 products), with FMA contraction OFF and correctly rounded div/sqrt (HIP defaults).
+// That is what makes radii / tiles_touched / sort keys / point lists / ranges bit-identical
+// to the CPU oracle (oracle/gsr_oracle.c), which restates the same upstream functions.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#pragma clang fp contract(off)
+
+#define GSR_TILE_X 16
+#define GSR_TILE_Y 16
+#define GSR_WAVE 64
+
+namespace gsr {
+
+// One visible Gaussian as the blend consumes it: 48 B, three 16-B loads, written by the
+// preprocess, gathered by tile lists.  a = {x, y, conic.a, conic.b}; b = {conic.c, opacity,
+// r, g}; c = {b, cull_ex, cull_ey, radius (int bits)}.
+struct alignas(16) SplatRecord {
+    float4 a, b, c;
+};
+
+__device__ __forceinline__ int f2i_sat(float v) {
+    // float -> int with CUDA cvt.rzi.s32.f32 semantics: truncate, saturate, NaN -> 0.
+    if (!(v == v)) return 0;
+    if (v >= 2147483648.0f) return 2147483647;
+    if (v <= -2147483648.0f) return (-2147483647 - 1);
+    return (int)v;
+}
+
+// --- upstream auxiliary.h --------------------------------------------------------------
+__device__ __forceinline__ float3 transform_point_4x3(float3 p, const float *M) {
+    float3 r;
+    r.x = M[0] * p.x + M[4] * p.y + M[8] * p.z + M[12];
+    r.y = M[1] * p.x + M[5] * p.y + M[9] * p.z + M[13];
+    r.z = M[2] * p.x + M[6] * p.y + M[10] * p.z + M[14];
+    return r;
+}
+
+__device__ __forceinline__ float4 transform_point_4x4(float3 p, const float *M) {
+    float4 r;
+    r.x = M[0] * p.x + M[4] * p.y + M[8] * p.z + M[12];
+    r.y = M[1] * p.x + M[5] * p.y + M[9] * p.z + M[13];
+    r.z = M[2] * p.x + M[6] * p.y + M[10] * p.z + M[14];
+    r.w = M[3] * p.x + M[7] * p.y + M[11] * p.z + M[15];
+    return r;
+}
+
+// upstream ndc2Pix: `((v + 1.0) * S - 1.0) * 0.5` -- the literals are double.
+__device__ __forceinline__ float ndc2pix(float v, int S) {
+    return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5);
+}
+
+struct Rect {
+    uint32_t x0, y0, x1, y1;
+};
+
+__device__ __forceinline__ Rect get_rect(float px, float py, int r, uint32_t gx, uint32_t gy) {
+    Rect q;
+    q.x0 = min(gx, (uint32_t)max(0, f2i_sat((px - r) / GSR_TILE_X)));
+    q.y0 = min(gy, (uint32_t)max(0, f2i_sat((py - r) / GSR_TILE_Y)));
+    q.x1 = min(gx, (uint32_t)max(0, f2i_sat((px + r + GSR_TILE_X - 1) / GSR_TILE_X)));
+    q.y1 = min(gy, (uint32_t)max(0, f2i_sat((py + r + GSR_TILE_Y - 1) / GSR_TILE_Y)));
+    return q;
+}
+
+// --- glm-style 3x3, column-major m[col][row] -------------------------------------------
+struct Mat3 {
+    float m[3][3];
+};
+
+__device__ __forceinline__ Mat3 mat3_cols(float a0, float a1, float a2, float a3, float a4,
+                                          float a5, float a6, float a7, float a8) {
+    Mat3 r;
+    r.m[0][0] = a0; r.m[0][1] = a1; r.m[0][2] = a2;
+    r.m[1][0] = a3; r.m[1][1] = a4; r.m[1][2] = a5;
+    r.m[2][0] = a6; r.m[2][1] = a7; r.m[2][2] = a8;
+    return r;
+}
+
+__device__ __forceinline__ Mat3 mat3_mul(const Mat3 &a, const Mat3 &b) {
+    Mat3 r;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            float s = a.m[0][i] * b.m[j][0];
+            s = s + a.m[1][i] * b.m[j][1];
+            s = s + a.m[2][i] * b.m[j][2];
+            r.m[j][i] = s;
+        }
+    return r;
+}
+
+__device__ __forceinline__ Mat3 mat3_transpose(const Mat3 &a) {
+    Mat3 r;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) r.m[i][j] = a.m[j][i];
+    return r;
+}
+
+// upstream forward.cu computeCov3D (twin: shaders/gau_vert.glsl:73-93)
+__device__ __forceinline__ void compute_cov3d(float3 s, float mod, float4 q, float c[6]) {
+    Mat3 S = mat3_cols(1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f);
+    S.m[0][0] = mod * s.x;
+    S.m[1][1] = mod * s.y;
+    S.m[2][2] = mod * s.z;
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    Mat3 R = mat3_cols(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                       2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                       2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+    Mat3 M = mat3_mul(S, R);
+    Mat3 Mt = mat3_transpose(M);
+    Mat3 Sig = mat3_mul(Mt, M);
+    c[0] = Sig.m[0][0];
+    c[1] = Sig.m[0][1];
+    c[2] = Sig.m[0][2];
+    c[3] = Sig.m[1][1];
+    c[4] = Sig.m[1][2];
+    c[5] = Sig.m[2][2];
+}
+
+// upstream forward.cu computeCov2D (twin: shaders/gau_vert.glsl:95-120).  `t` is the
+// view-space mean (transformPoint4x3(mean, viewmatrix), already computed by the caller).
+__device__ __forceinline__ float3 compute_cov2d(float3 t, float fx, float fy, float tanfovx,
+                                                float tanfovy, const float c[6], const float *vm) {
+    const float limx = 1.3f * tanfovx;
+    const float limy = 1.3f * tanfovy;
+    const float txtz = t.x / t.z;
+    const float tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    Mat3 J = mat3_cols(fx / t.z, 0.0f, -(fx * t.x) / (t.z * t.z), 0.0f, fy / t.z,
+                       -(fy * t.y) / (t.z * t.z), 0.f, 0.f, 0.f);
+    Mat3 W = mat3_cols(vm[0], vm[4], vm[8], vm[1], vm[5], vm[9], vm[2], vm[6], vm[10]);
+    Mat3 T = mat3_mul(W, J);
+    Mat3 Vrk = mat3_cols(c[0], c[1], c[2], c[1], c[3], c[4], c[2], c[4], c[5]);
+    Mat3 Tt = mat3_transpose(T);
+    Mat3 Vt = mat3_transpose(Vrk);
+    Mat3 A = mat3_mul(Tt, Vt);
+    Mat3 cov = mat3_mul(A, T);
+    cov.m[0][0] += 0.3f;
+    cov.m[1][1] += 0.3f;
+    return make_float3(cov.m[0][0], cov.m[0][1], cov.m[1][1]);
+}
+
+// Order-preserving float -> uint32 key for a general float sort (negatives, -0 == +0,
+// every NaN last): stable radix on these keys == np.argsort(kind='stable').
+__device__ __forceinline__ uint32_t float_sort_key(float f) {
+    uint32_t u = __float_as_uint(f);
+    if (f == 0.0f) u = 0u;
+    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    if (f != f) u = 0xFFFFFFFFu;
+    return u;
+}
+
+// --- wave / block scans (256-thread blocks, wave64) ------------------------------------
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+
+// Exclusive scan over a 256-thread block.  s_tmp: 4 words of LDS.  Returns the exclusive
+// prefix of `v` and the block total in `total`.  Contains two barriers.
+__device__ __forceinline__ uint32_t block256_exclusive_scan(uint32_t v, uint32_t *s_tmp,
+                                                            uint32_t &total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t inc = wave_inclusive_scan(v);
+    if (lane == 63) s_tmp[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t t = s_tmp[i];
+        pre += (i < w) ? t : 0u;
+        tot += t;
+    }
+    __syncthreads();
+    total = tot;
+    return pre + inc - v;
+}
+
+}  // namespace gsr
+
+// ---- host-side launchers (defined in the .hip files, called by api.hip) ------------------
+struct GsrPreprocessArgs {
+    int64_t P;
+    int D, M;
+    float scale_modifier;
+    const float *means3D, *scales, *rotations, *opacities, *shs, *colors_precomp, *cov3D_precomp;
+    const float *viewmatrix, *projmatrix, *campos;
+    float tanfovx, tanfovy, focal_x, focal_y;
+    int W, H;
+    uint32_t grid_x, grid_y, row_begin, row_end;
+    int prefiltered;
+    int sh_vec4, rot_vec4;  // 16-B aligned rows: vector loads allowed
+    // workspace outputs
+    int32_t *radii;
+    gsr::SplatRecord *records;
+    uint32_t *sort_keys, *sort_vals, *strip_tiles;
+    // optional debug outputs
+    float *depths, *means2D, *conic_opacity, *rgb;
+    uint32_t *tiles_touched;
+};
+
+hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, hipStream_t s);
+hipError_t gsr_launch_mark_visible(const float *means3D, int64_t P, const float *viewmatrix,
+                                   uint8_t *visible, hipStream_t s);
+hipError_t gsr_launch_view_depth_keys(const float *xyz, int64_t P, float v20, float v21, float v22,
+                                      float v23, uint32_t *keys, uint32_t *vals, float *depth_out,
+                                      hipStream_t s);
+hipError_t gsr_launch_index_to_i32(const uint32_t *vals, int64_t P, int32_t *out, hipStream_t s);
+
+// Radix sort of (uint32 key, uint32 value) pairs, stable, LSD over key bits [begin, end).
+// On return *keys / *vals point at the buffers holding the sorted data (either the input
+// pair or the alt pair).  hist needs gsr_radix_hist_words(n) words.
+int64_t gsr_radix_hist_words(int64_t n);
+hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
+                                uint32_t **vals_alt, int64_t n, int begin_bit, int end_bit,
+                                uint32_t *hist, uint32_t *digit_total, hipStream_t s);
+
+// Binning: offsets scan over depth-sorted strip tile counts, duplicate into (tile, id)
+// pairs, and tile ranges.
+int64_t gsr_scan_blocks(int64_t n);
+hipError_t gsr_launch_scan_reduce(const uint32_t *perm, const uint32_t *strip_tiles, int64_t n,
+                                  uint32_t *partials, hipStream_t s);
+hipError_t gsr_launch_scan_partials(uint32_t *partials, int64_t nb, uint64_t *total,
+                                    hipStream_t s);
+hipError_t gsr_launch_duplicate(const uint32_t *perm, const uint32_t *strip_tiles,
+                                const uint32_t *partials, int64_t n,
+                                const gsr::SplatRecord *records, uint32_t gx, uint32_t gy,
+                                uint32_t row_begin, uint32_t row_end, uint32_t *tile_keys,
+                                uint32_t *tile_vals, hipStream_t s);
+hipError_t gsr_launch_ranges(const uint32_t *tile_keys, int64_t K, uint32_t *ranges,
+                             hipStream_t s);
+hipError_t gsr_launch_globalize_tiles(const uint32_t *local, int64_t K, uint32_t offset,
+                                      uint32_t *global, hipStream_t s);
+
+struct GsrBlendArgs {
+    const uint2 *ranges;  // strip-local tile ranges
+    const uint32_t *point_list;
+    const gsr::SplatRecord *records;
+    int W, H;
+    uint32_t grid_x, row_begin, rows_tiles;
+    int y0, rows_out;
+    const float *bg;
+    float *out_color, *final_T;
+    uint32_t *n_contrib;
+    int cull;
+};
+hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s);

@@ -1,0 +1,266 @@
+// preprocess.hip -- per-Gaussian EWA projection + SH -> RGB (gfx950).
+//
+// Replaces upstream diff-gaussian-rasterization forward.cu preprocessCUDA (called from
+// renderer_cuda.py:215 via GaussianRasterizer.forward) and auxiliary.h in_frustum.
+// One thread per Gaussian, 256-thread blocks (4 waves).  HBM-bound: per Gaussian it reads
+// xyz (12 B) for every point, scale/rot/opacity (32 B) for points in front of the camera
+// and SH (192 B at degree 3) only for points that survive culling; it writes one 48-B
+// SplatRecord for visible points plus the 8-B (key, id) pair of the depth sort and 8 B of
+// radius / strip tile count.
+#include "gsr_internal.h"
+
+using namespace gsr;
+
+namespace {
+
+__constant__ float kShC0 = 0.28209479177387814f;
+__constant__ float kShC1 = 0.4886025119029199f;
+__constant__ float kShC2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+                               -1.0925484305920792f, 0.5462742152960396f};
+__constant__ float kShC3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                               0.3731763325901154f, -0.4570457994644658f, 1.445305721320277f,
+                               -0.5900435899266435f};
+
+// upstream forward.cu computeColorFromSH (twin: shaders/gau_vert.glsl:213-250), but with the
+// coefficients read as 16-B vectors: the (P, M, 3) row of one Gaussian is 192 B = 12 float4
+// at degree 3 (M = 16), so each lane issues 12 dwordx4 loads instead of 48 dword loads.
+__device__ __forceinline__ float3 color_from_sh(float3 pos, const float *campos, const float *sh,
+                                                int deg, bool vec_ok) {
+    float dx = pos.x - campos[0], dy = pos.y - campos[1], dz = pos.z - campos[2];
+    const float len = sqrtf(dx * dx + dy * dy + dz * dz);
+    dx = dx / len;
+    dy = dy / len;
+    dz = dz / len;
+    // Load the coefficients this degree needs: (deg+1)^2 of the M stored (host checks
+    // (deg+1)^2 <= M).  Both loops are fully unrolled so `c` stays in registers.
+    float c[48];
+    const int ncoef = (deg + 1) * (deg + 1);
+    if (vec_ok) {  // M == 16 and 16-B aligned rows
+        const float4 *v = reinterpret_cast<const float4 *>(sh);
+        const int nvec = (ncoef * 3 + 3) >> 2;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+            float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (i < nvec) q = v[i];
+            c[4 * i + 0] = q.x;
+            c[4 * i + 1] = q.y;
+            c[4 * i + 2] = q.z;
+            c[4 * i + 3] = q.w;
+        }
+    } else {
+        const int nflt = ncoef * 3;
+#pragma unroll
+        for (int i = 0; i < 48; ++i) c[i] = (i < nflt) ? sh[i] : 0.0f;
+    }
+    float r0 = kShC0 * c[0], r1 = kShC0 * c[1], r2 = kShC0 * c[2];
+    if (deg > 0) {
+        const float x = dx, y = dy, z = dz;
+        const float a1 = kShC1 * y, a2 = kShC1 * z, a3 = kShC1 * x;
+        r0 = r0 - a1 * c[3] + a2 * c[6] - a3 * c[9];
+        r1 = r1 - a1 * c[4] + a2 * c[7] - a3 * c[10];
+        r2 = r2 - a1 * c[5] + a2 * c[8] - a3 * c[11];
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z;
+            const float xy = x * y, yz = y * z, xz = x * z;
+            const float b0 = kShC2[0] * xy;
+            const float b1 = kShC2[1] * yz;
+            const float b2 = kShC2[2] * (2.0f * zz - xx - yy);
+            const float b3 = kShC2[3] * xz;
+            const float b4 = kShC2[4] * (xx - yy);
+            r0 = r0 + b0 * c[12] + b1 * c[15] + b2 * c[18] + b3 * c[21] + b4 * c[24];
+            r1 = r1 + b0 * c[13] + b1 * c[16] + b2 * c[19] + b3 * c[22] + b4 * c[25];
+            r2 = r2 + b0 * c[14] + b1 * c[17] + b2 * c[20] + b3 * c[23] + b4 * c[26];
+            if (deg > 2) {
+                const float e0 = kShC3[0] * y * (3.0f * xx - yy);
+                const float e1 = kShC3[1] * xy * z;
+                const float e2 = kShC3[2] * y * (4.0f * zz - xx - yy);
+                const float e3 = kShC3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
+                const float e4 = kShC3[4] * x * (4.0f * zz - xx - yy);
+                const float e5 = kShC3[5] * z * (xx - yy);
+                const float e6 = kShC3[6] * x * (xx - 3.0f * yy);
+                r0 = r0 + e0 * c[27] + e1 * c[30] + e2 * c[33] + e3 * c[36] + e4 * c[39] +
+                     e5 * c[42] + e6 * c[45];
+                r1 = r1 + e0 * c[28] + e1 * c[31] + e2 * c[34] + e3 * c[37] + e4 * c[40] +
+                     e5 * c[43] + e6 * c[46];
+                r2 = r2 + e0 * c[29] + e1 * c[32] + e2 * c[35] + e3 * c[38] + e4 * c[41] +
+                     e5 * c[44] + e6 * c[47];
+            }
+        }
+    }
+    r0 += 0.5f;
+    r1 += 0.5f;
+    r2 += 0.5f;
+    return make_float3(fmaxf(r0, 0.0f), fmaxf(r1, 0.0f), fmaxf(r2, 0.0f));
+}
+
+// Conservative half-extents (pixels) of the region where this splat can reach
+// alpha >= 1/255: o*exp(power) >= 1/255  <=>  q(d) = A dx^2 + 2B dx dy + C dy^2 <= 2 ln(255 o).
+// The box is computed in double from the float conic the blend evaluates, widened by an
+// absolute bound on the float rounding of `power` and by a pixel margin.  It is only used
+// by the blend to skip whole waves; outputs are identical with and without it (tested).
+__device__ __forceinline__ float2 cull_extent(float A, float B, float C, float o) {
+    const float kInf = __builtin_huge_valf();
+    const double det = (double)A * (double)C - (double)B * (double)B;
+    if (!(det > 0.0) || !(A > 0.0f) || !(C > 0.0f) || !(o == o)) return make_float2(kInf, kInf);
+    double L = log(255.0 * (double)o);
+    if (L < 0.0) L = 0.0;
+    const double sxx = (double)C / det, syy = (double)A / det;  // inverse of the conic
+    double ex = sqrt(2.0 * L * sxx), ey = sqrt(2.0 * L * syy);
+    // |float(power) - power| <= ~8 eps (|A|dx^2 + |C|dy^2 + 2|B dx dy|) inside the box.
+    const double mag = ((double)A + (double)C + 2.0 * fabs((double)B)) * (ex * ex + ey * ey);
+    const double Lm = (L + 8.0 * 5.96e-8 * mag + 1e-3) * 1.01;
+    ex = sqrt(2.0 * Lm * sxx) + 0.02;
+    ey = sqrt(2.0 * Lm * syy) + 0.02;
+    if (!(ex < 1e30) || !(ey < 1e30)) return make_float2(kInf, kInf);
+    return make_float2((float)ex, (float)ey);
+}
+
+__global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    int32_t radius_out = 0;
+    uint32_t strip_tiles = 0, all_tiles = 0;
+    uint32_t key = 0xFFFFFFFFu;
+
+    const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1],
+                                 a.means3D[3 * idx + 2]);
+    const float3 p_view = transform_point_4x3(p, a.viewmatrix);
+    if (p_view.z > 0.2f) {  // in_frustum
+        const float4 p_hom = transform_point_4x4(p, a.projmatrix);
+        const float p_w = 1.0f / (p_hom.w + 0.0000001f);
+        const float p_proj_x = p_hom.x * p_w, p_proj_y = p_hom.y * p_w;
+
+        float cov3d[6];
+        if (a.cov3D_precomp) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) cov3d[i] = a.cov3D_precomp[6 * idx + i];
+        } else {
+            const float3 s = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1],
+                                         a.scales[3 * idx + 2]);
+            const float4 q = a.rot_vec4 ? reinterpret_cast<const float4 *>(a.rotations)[idx]
+                                        : make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1],
+                                                      a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
+            compute_cov3d(s, a.scale_modifier, q, cov3d);
+        }
+        const float3 cov = compute_cov2d(p_view, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy,
+                                         cov3d, a.viewmatrix);
+        const float det = cov.x * cov.z - cov.y * cov.y;
+        if (det != 0.0f) {
+            const float det_inv = 1.f / det;
+            const float conic_a = cov.z * det_inv, conic_b = -cov.y * det_inv,
+                        conic_c = cov.x * det_inv;
+            const float mid = 0.5f * (cov.x + cov.z);
+            const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+            const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+            const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
+            const float px = ndc2pix(p_proj_x, a.W), py = ndc2pix(p_proj_y, a.H);
+            const int r_int = f2i_sat(my_radius);
+            const Rect rc = get_rect(px, py, r_int, a.grid_x, a.grid_y);
+            all_tiles = (rc.x1 - rc.x0) * (rc.y1 - rc.y0);
+            if (all_tiles != 0) {
+                float3 col;
+                if (a.colors_precomp) {
+                    col = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1],
+                                      a.colors_precomp[3 * idx + 2]);
+                } else {
+                    col = color_from_sh(p, a.campos, a.shs + idx * (int64_t)a.M * 3, a.D, a.sh_vec4);
+                }
+                const float opacity = a.opacities[idx];
+                radius_out = r_int;
+                const uint32_t sy0 = max(rc.y0, a.row_begin), sy1 = min(rc.y1, a.row_end);
+                strip_tiles = sy1 > sy0 ? (rc.x1 - rc.x0) * (sy1 - sy0) : 0u;
+                if (strip_tiles) key = __float_as_uint(p_view.z);  // z > 0.2: bits are monotone
+                const float2 ext = cull_extent(conic_a, conic_b, conic_c, opacity);
+                SplatRecord rec;
+                rec.a = make_float4(px, py, conic_a, conic_b);
+                rec.b = make_float4(conic_c, opacity, col.x, col.y);
+                rec.c = make_float4(col.z, ext.x, ext.y, __int_as_float(r_int));
+                a.records[idx] = rec;
+                if (a.depths) a.depths[idx] = p_view.z;
+                if (a.means2D) {
+                    a.means2D[2 * idx] = px;
+                    a.means2D[2 * idx + 1] = py;
+                }
+                if (a.conic_opacity)
+                    reinterpret_cast<float4 *>(a.conic_opacity)[idx] =
+                        make_float4(conic_a, conic_b, conic_c, opacity);
+                if (a.rgb && !a.colors_precomp) {
+                    a.rgb[3 * idx] = col.x;
+                    a.rgb[3 * idx + 1] = col.y;
+                    a.rgb[3 * idx + 2] = col.z;
+                }
+            }
+        }
+    }
+    a.radii[idx] = radius_out;
+    a.strip_tiles[idx] = strip_tiles;
+    a.sort_keys[idx] = key;
+    a.sort_vals[idx] = (uint32_t)idx;
+    if (a.tiles_touched) a.tiles_touched[idx] = strip_tiles;
+}
+
+// GaussianRasterizer.markVisible -> upstream markVisible kernel: in_frustum only.
+__global__ __launch_bounds__(256) void k_mark_visible(const float *__restrict__ means3D,
+                                                      int64_t P, const float *viewmatrix,
+                                                      uint8_t *visible) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    const float3 p = make_float3(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
+    visible[idx] = transform_point_4x3(p, viewmatrix).z > 0.2f ? 1 : 0;
+}
+
+// Depth-sort backend (renderer_ogl.py:10-19): view-space z of each point in the operation
+// order the reference's numpy stacked matmul produced in the build container
+// (fma(v22, z, fma(v20, x, v21*y)) + v23), then an order-preserving
+// uint32 key so the stable radix sort returns np.argsort(depth, kind='stable').
+__global__ __launch_bounds__(256) void k_view_depth_keys(const float *__restrict__ xyz, int64_t P,
+                                                         float v20, float v21, float v22, float v23,
+                                                         uint32_t *keys, uint32_t *vals,
+                                                         float *depth_out) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    const float x = xyz[3 * idx], y = xyz[3 * idx + 1], z = xyz[3 * idx + 2];
+    const float d = __builtin_fmaf(v22, z, __builtin_fmaf(v20, x, v21 * y)) + v23;
+    keys[idx] = float_sort_key(d);
+    vals[idx] = (uint32_t)idx;
+    if (depth_out) depth_out[idx] = d;
+}
+
+__global__ __launch_bounds__(256) void k_index_to_i32(const uint32_t *vals, int64_t P,
+                                                      int32_t *out) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx < P) out[idx] = (int32_t)vals[idx];
+}
+
+inline unsigned grid_for(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+}  // namespace
+
+hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, hipStream_t s) {
+    if (a.P == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_preprocess, dim3(grid_for(a.P)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t gsr_launch_mark_visible(const float *means3D, int64_t P, const float *viewmatrix,
+                                   uint8_t *visible, hipStream_t s) {
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mark_visible, dim3(grid_for(P)), dim3(256), 0, s, means3D, P, viewmatrix,
+                       visible);
+    return hipGetLastError();
+}
+
+hipError_t gsr_launch_view_depth_keys(const float *xyz, int64_t P, float v20, float v21, float v22,
+                                      float v23, uint32_t *keys, uint32_t *vals, float *depth_out,
+                                      hipStream_t s) {
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_view_depth_keys, dim3(grid_for(P)), dim3(256), 0, s, xyz, P, v20, v21,
+                       v22, v23, keys, vals, depth_out);
+    return hipGetLastError();
+}
+
+hipError_t gsr_launch_index_to_i32(const uint32_t *vals, int64_t P, int32_t *out, hipStream_t s) {
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_index_to_i32, dim3(grid_for(P)), dim3(256), 0, s, vals, P, out);
+    return hipGetLastError();
+}

@@ -1,0 +1,226 @@
+"""Drop-in replacement for the `diff_gaussian_rasterization` Python API the viewer imports.
+
+renderer_cuda.py:13 does `from diff_gaussian_rasterization import GaussianRasterizationSettings,
+GaussianRasterizer` and renderer_cuda.py:211-224 calls
+
+    GaussianRasterizer(raster_settings=GaussianRasterizationSettings(**settings))(
+        means3D=..., means2D=None, shs=..., colors_precomp=None, opacities=...,
+        scales=..., rotations=..., cov3D_precomp=None)  ->  (color [3,H,W], radii [P])
+
+The names, field order, argument checks and return values below follow that third-party API
+(upstream `diff_gaussian_rasterization/__init__.py` and `_C.rasterize_gaussians` in
+rasterize_points.cu); the work is done by libgsr.so (HIP, gfx950) through `_lib`.
+Forward only: the viewer never differentiates (renderer_cuda.py:214 `torch.no_grad()`).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import NamedTuple
+
+import torch
+
+from . import _lib
+
+
+class GaussianRasterizationSettings(NamedTuple):
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    bg: torch.Tensor
+    scale_modifier: float
+    viewmatrix: torch.Tensor
+    projmatrix: torch.Tensor
+    sh_degree: int
+    campos: torch.Tensor
+    prefiltered: bool
+    debug: bool
+
+
+def _device_of(t: torch.Tensor) -> torch.device:
+    if not t.is_cuda:
+        raise RuntimeError("means3D must be a device (HIP) tensor")
+    return t.device
+
+
+def _as_dev(t, device, shape_hint: str):
+    if t is None:
+        return None
+    if not isinstance(t, torch.Tensor):
+        t = torch.as_tensor(t)
+    if t.numel() == 0:
+        return None
+    if t.device != device:
+        t = t.to(device)
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
+
+
+class ForwardResult(NamedTuple):
+    """Everything one native forward produced (color/radii plus optional intermediates)."""
+    num_rendered: int
+    color: torch.Tensor
+    radii: torch.Tensor
+    extras: dict
+
+
+def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, rotations,
+                               scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tanfovx,
+                               tanfovy, image_height, image_width, sh, degree, campos, prefiltered,
+                               debug, *, tile_rows=None, extras=(), stream=None) -> ForwardResult:
+    """Same arguments, order and validation as upstream `_C.rasterize_gaussians`.
+
+    Extensions (keyword-only, for the strip partition and the parity tests):
+      tile_rows -- (begin, end) 16-px tile rows to render; the image is then strip-local;
+      extras    -- names of intermediates to return: depths, means2D, conic_opacity, rgb,
+                   tiles_touched, final_T, n_contrib.
+    """
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    device = _device_of(means3D)
+    dev_index = device.index if device.index is not None else torch.cuda.current_device()
+    P = int(means3D.size(0))
+    H, W = int(image_height), int(image_width)
+    means3D = _as_dev(means3D, device, "P,3")
+    opacities = _as_dev(opacities, device, "P,1")
+    scales = _as_dev(scales, device, "P,3")
+    rotations = _as_dev(rotations, device, "P,4")
+    cov3D_precomp = _as_dev(cov3D_precomp, device, "P,6")
+    colors_precomp = _as_dev(colors_precomp, device, "P,3")
+    sh = _as_dev(sh, device, "P,M,3")
+    bg = _as_dev(bg, device, "3")
+    viewmatrix = _as_dev(viewmatrix, device, "4,4")
+    projmatrix = _as_dev(projmatrix, device, "4,4")
+    campos = _as_dev(campos, device, "3")
+
+    M = 0
+    if sh is not None:
+        M = int(sh.size(1)) if sh.ndimension() == 3 else int(sh.numel() // max(P, 1) // 3)
+
+    gy = (H + 15) // 16
+    if tile_rows is None:
+        rb, re = 0, 0
+        y0, rows = 0, H
+    else:
+        rb, re = int(tile_rows[0]), int(tile_rows[1])
+        y0 = rb * 16
+        rows = min(H, re * 16) - y0
+        if not (0 <= rb < re <= gy):
+            raise RuntimeError(f"tile_rows {tile_rows} outside [0, {gy}]")
+
+    f32 = dict(dtype=torch.float32, device=device)
+    color = torch.empty((3, rows, W), **f32)
+    radii = torch.empty((P,), dtype=torch.int32, device=device)
+    ext = {}
+    for name in extras:
+        if name == "depths":
+            ext[name] = torch.zeros((P,), **f32)
+        elif name == "means2D":
+            ext[name] = torch.zeros((P, 2), **f32)
+        elif name == "conic_opacity":
+            ext[name] = torch.zeros((P, 4), **f32)
+        elif name == "rgb":
+            ext[name] = torch.zeros((P, 3), **f32)
+        elif name == "tiles_touched":
+            ext[name] = torch.zeros((P,), dtype=torch.int32, device=device)
+        elif name == "final_T":
+            ext[name] = torch.zeros((rows, W), **f32)
+        elif name == "n_contrib":
+            ext[name] = torch.zeros((rows, W), dtype=torch.int32, device=device)
+        else:
+            raise ValueError(f"unknown extra output {name!r}")
+
+    g = _lib.GsrGaussians(P=P, D=int(degree), M=M, scale_modifier=float(scale_modifier),
+                          means3D=_lib.ptr(means3D), scales=_lib.ptr(scales),
+                          rotations=_lib.ptr(rotations), opacities=_lib.ptr(opacities),
+                          shs=_lib.ptr(sh), colors_precomp=_lib.ptr(colors_precomp),
+                          cov3D_precomp=_lib.ptr(cov3D_precomp))
+    st = _lib.GsrRasterSettings(image_width=W, image_height=H, tanfovx=float(tanfovx),
+                                tanfovy=float(tanfovy), viewmatrix=_lib.ptr(viewmatrix),
+                                projmatrix=_lib.ptr(projmatrix), campos=_lib.ptr(campos),
+                                bg=_lib.ptr(bg), tile_row_begin=rb, tile_row_end=re,
+                                prefiltered=int(bool(prefiltered)), debug=int(bool(debug)))
+    out = _lib.GsrOutputs(color=color.data_ptr(), radii=radii.data_ptr() if P else None)
+    for name, t in ext.items():
+        setattr(out, name, t.data_ptr())
+    if stream is None:
+        stream = torch.cuda.current_stream(device).cuda_stream
+    lib = _lib.load_library()
+    ctx = _lib.context(dev_index)
+    with torch.cuda.device(dev_index):
+        _lib.check(lib.gsr_forward(ctx, ctypes.byref(g), ctypes.byref(st), ctypes.byref(out),
+                                   ctypes.c_void_p(stream)), "gsr_forward")
+    return ForwardResult(int(out.num_rendered), color, radii, ext)
+
+
+def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
+                        cov3Ds_precomp, raster_settings: GaussianRasterizationSettings):
+    """upstream rasterize_gaussians(...) -> (color, radii)."""
+    del means2D  # only carries screen-space gradients upstream
+    res = rasterize_gaussians_native(
+        raster_settings.bg, means3D, colors_precomp, opacities, scales, rotations,
+        raster_settings.scale_modifier, cov3Ds_precomp, raster_settings.viewmatrix,
+        raster_settings.projmatrix, raster_settings.tanfovx, raster_settings.tanfovy,
+        raster_settings.image_height, raster_settings.image_width, sh, raster_settings.sh_degree,
+        raster_settings.campos, raster_settings.prefiltered, raster_settings.debug)
+    return res.color, res.radii
+
+
+class GaussianRasterizer(torch.nn.Module):
+    def __init__(self, raster_settings: GaussianRasterizationSettings):
+        super().__init__()
+        self.raster_settings = raster_settings
+
+    def markVisible(self, positions: torch.Tensor) -> torch.Tensor:
+        """Frustum-cull test per point: view-space z > 0.2 (upstream markVisible)."""
+        with torch.no_grad():
+            rs = self.raster_settings
+            device = _device_of(positions)
+            positions = _as_dev(positions, device, "P,3")
+            P = int(positions.size(0)) if positions is not None else 0
+            visible = torch.zeros((P,), dtype=torch.bool, device=device)
+            if P == 0:
+                return visible
+            view = _as_dev(rs.viewmatrix, device, "4,4")
+            proj = _as_dev(rs.projmatrix, device, "4,4")
+            idx = device.index if device.index is not None else torch.cuda.current_device()
+            lib = _lib.load_library()
+            with torch.cuda.device(idx):
+                _lib.check(lib.gsr_mark_visible(
+                    _lib.context(idx), positions.data_ptr(), P, view.data_ptr(),
+                    proj.data_ptr(), visible.data_ptr(),
+                    ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)),
+                    "gsr_mark_visible")
+            return visible
+
+    def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None,
+                rotations=None, cov3D_precomp=None):
+        rs = self.raster_settings
+        if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
+            raise Exception('Please provide excatly one of either SHs or precomputed colors!')
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or \
+                ((scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception('Please provide exactly one of either scale/rotation pair or '
+                            'precomputed 3D covariance!')
+        return rasterize_gaussians(means3D, means2D, shs, colors_precomp, opacities, scales,
+                                   rotations, cov3D_precomp, rs)
+
+
+def binning_state(device_index: int = 0):
+    """(point_list, point_tiles, ranges [T,2]) of the last forward on a device, as device
+    int32 tensors holding the uint32 values (test / debug helper)."""
+    lib = _lib.load_library()
+    ctx = _lib.context(device_index)
+    K = ctypes.c_int64()
+    T = ctypes.c_int32()
+    stream = ctypes.c_void_p(torch.cuda.current_stream(device_index).cuda_stream)
+    _lib.check(lib.gsr_get_binning(ctx, None, None, None, ctypes.byref(K), ctypes.byref(T),
+                                   stream), "gsr_get_binning")
+    dev = torch.device("cuda", device_index)
+    pl = torch.empty((K.value,), dtype=torch.int32, device=dev)
+    pt = torch.empty((K.value,), dtype=torch.int32, device=dev)
+    rg = torch.empty((T.value, 2), dtype=torch.int32, device=dev)
+    _lib.check(lib.gsr_get_binning(ctx, _lib.ptr(pl), _lib.ptr(pt), _lib.ptr(rg), None, None,
+                                   stream), "gsr_get_binning")
+    return pl, pt, rg

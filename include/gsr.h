@@ -1,0 +1,146 @@
+/*
+ * gsr.h -- C ABI of the MI355X-native forward Gaussian-splat rasterizer (libgsr.so).
+ *
+ * This is the drop-in boundary under the viewer's CUDA backend.  Every entry point names
+ * the reference interface it replaces (paths relative to /root/reference):
+ *
+ *   gsr_forward        <- diff_gaussian_rasterization `_C.rasterize_gaussians(...)` as called
+ *                         by GaussianRasterizer.forward, which renderer_cuda.py:211-224
+ *                         (CUDARenderer.draw) invokes every frame.  [third-party, un-vendored]
+ *   gsr_mark_visible   <- `_C.mark_visible(positions, viewmatrix, projmatrix)` behind
+ *                         GaussianRasterizer.markVisible.  [third-party, un-vendored]
+ *   gsr_depth_argsort  <- the per-frame depth sort backend `_sort_gaussian(gaus, view_mat)`
+ *                         (renderer_ogl.py:10-19 cpu, :22-38 cupy, :41-53 torch), consumed by
+ *                         OpenGLRenderer.sort_and_update (renderer_ogl.py:139-146).
+ *
+ * Conventions (plain pointers and sizes only; no torch or HIP types):
+ *   - every array pointer is DEVICE memory unless the comment says host;
+ *   - matrices passed as device pointers are 16 floats, column-major (upstream's layout,
+ *     i.e. the row-major bytes of `view.T` that renderer_cuda.py:192-194 uploads);
+ *   - `stream` is a hipStream_t (NULL = the default stream); all work is enqueued on it.
+ *     gsr_forward synchronises that stream once per call to read back the number of
+ *     (Gaussian, tile) pairs, as upstream does for num_rendered;
+ *   - every function returns GSR_OK (0) or a negative GSR_E* code; gsr_last_error()
+ *     returns the calling thread's last message.  The Python layer raises RuntimeError.
+ */
+#ifndef GSR_H
+#define GSR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSR_ABI_VERSION 1
+
+enum {
+    GSR_OK = 0,
+    GSR_E_INVALID = -1, /* bad argument / shape */
+    GSR_E_HIP = -2,     /* a HIP runtime call or kernel failed */
+    GSR_E_NOMEM = -3,   /* device allocation failed */
+    GSR_E_STATE = -4    /* call order (e.g. no forward yet) */
+};
+
+typedef struct gsr_context gsr_context; /* device workspace + stage events; one per device */
+
+/* Gaussians: the five tensors of GaussianDataCUDA (renderer_cuda.py:55-68, built by
+ * gaus_cuda_from_cpu :87-98), contiguous float32.  Exactly one of {shs, colors_precomp} and
+ * exactly one of {(scales, rotations), cov3D_precomp} must be non-NULL. */
+typedef struct {
+    int64_t P;            /* number of Gaussians */
+    int32_t D;            /* active SH degree (raster_settings["sh_degree"], :137) */
+    int32_t M;            /* SH coefficients stored per Gaussian = shs.size(1) (16 or 1) */
+    float scale_modifier; /* raster_settings["scale_modifier"] */
+    const float *means3D;        /* [P,3]  */
+    const float *scales;         /* [P,3]  (already exp-activated, util_gau.py:118-119) */
+    const float *rotations;      /* [P,4]  quaternion (r,x,y,z), normalised by the loader */
+    const float *opacities;      /* [P,1]  (sigmoid-activated) */
+    const float *shs;            /* [P,M,3] */
+    const float *colors_precomp; /* [P,3]  */
+    const float *cov3D_precomp;  /* [P,6]  upper triangle xx,xy,xz,yy,yz,zz */
+} gsr_gaussians;
+
+/* GaussianRasterizationSettings (renderer_cuda.py:104-117). */
+typedef struct {
+    int32_t image_width, image_height;
+    float tanfovx, tanfovy;
+    const float *viewmatrix;    /* device [16], column-major */
+    const float *projmatrix;     /* device [16], column-major (full projection * view) */
+    const float *campos;         /* device [3] */
+    const float *bg;             /* device [3] */
+    /* Image-space strip (multi-GPU partition): render only 16-px tile rows
+     * [tile_row_begin, tile_row_end).  0/0 = the whole frame.  Output images are then
+     * strip-local: [3, rows, W] with rows = min(H, 16*end) - 16*begin. */
+    int32_t tile_row_begin, tile_row_end;
+    int32_t prefiltered; /* upstream: points are known to be in the frustum */
+    int32_t debug;       /* synchronise + check after every stage */
+} gsr_raster_settings;
+
+typedef struct {
+    float *color;    /* required: [3, rows, W] float32 (CHW, as upstream out_color) */
+    int32_t *radii;  /* required: [P] int32 (0 = culled) */
+    /* optional per-Gaussian intermediates (NULL = not written) */
+    float *depths;        /* [P]   view-space z */
+    float *means2D;       /* [P,2] pixel-space centre */
+    float *conic_opacity; /* [P,4] inverse 2D covariance (a,b,c) + opacity */
+    float *rgb;           /* [P,3] SH-evaluated colour, clamped >= 0 */
+    uint32_t *tiles_touched; /* [P] tiles overlapped inside the rendered strip */
+    /* optional per-pixel outputs, strip-local like color */
+    float *final_T;     /* [rows, W] */
+    uint32_t *n_contrib; /* [rows, W] */
+    /* written by gsr_forward */
+    int64_t num_rendered; /* K: number of (Gaussian, tile) pairs in the strip */
+} gsr_outputs;
+
+int gsr_abi_version(void);
+const char *gsr_last_error(void);
+
+int gsr_create(gsr_context **out); /* binds to the calling thread's current HIP device */
+void gsr_destroy(gsr_context *ctx);
+
+/* Pre-size the workspace so that a timed loop never allocates (sizes are grown on demand
+ * otherwise).  P Gaussians, K pairs. */
+int gsr_reserve(gsr_context *ctx, int64_t P, int64_t K);
+
+/* Forward rasterization: preprocess (EWA projection + SH) -> device radix depth sort ->
+ * tile binning (scan + duplicate + radix tile sort + ranges) -> per-tile blend. */
+int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings *s,
+                gsr_outputs *out, void *stream);
+
+/* Binning state of the last gsr_forward on this context.  Writes the sizes (K pairs, T tiles
+ * of the whole frame) and, for each non-NULL caller-owned DEVICE buffer, copies:
+ * point_list[K] Gaussian ids sorted by (tile, depth); point_tiles[K] their global tile ids;
+ * ranges[2*T] = [start,end) per tile (tiles outside the strip stay 0,0, as upstream's memset
+ * leaves unused tiles).  Call once with NULL buffers to size them.  Synchronises `stream`. */
+int gsr_get_binning(gsr_context *ctx, uint32_t *point_list, uint32_t *point_tiles,
+                    uint32_t *ranges, int64_t *num_rendered, int32_t *num_tiles, void *stream);
+
+/* GaussianRasterizer.markVisible: visible[i] = view-space z > 0.2. */
+int gsr_mark_visible(gsr_context *ctx, const float *means3D, int64_t P, const float *viewmatrix,
+                     const float *projmatrix, uint8_t *visible, void *stream);
+
+/* Depth-sort backend (renderer_ogl.py:10-19): depth = (view @ [xyz,1]).z with `view` the HOST
+ * 4x4 row-major (math-layout) matrix the viewer passes; out_index[P] int32 = stable ascending
+ * argsort of depth (== np.argsort(depth, kind='stable')).  out_depth[P] optional. */
+int gsr_depth_argsort(gsr_context *ctx, const float *xyz, int64_t P, const float *view_host16,
+                      int32_t *out_index, float *out_depth, void *stream);
+
+/* Stage timing (HIP events on the forward's stream, no extra synchronisation).
+ * gsr_set_timing(1) starts recording one event set per forward (a ring of the last 256);
+ * gsr_stage_times waits for the last timed forward and writes the MEAN per-stage time (ms)
+ * over the recorded forwards into ms[i] for i < n; it returns the number of stages.
+ * Stage names via gsr_stage_name(i). */
+int gsr_set_timing(gsr_context *ctx, int enable);
+int gsr_stage_times(gsr_context *ctx, float *ms, int n);
+const char *gsr_stage_name(int i);
+
+/* Tuning / verification switches.  GSR_OPT_BLEND_CULL (default 1): per-wave conservative
+ * ellipse cull in the blend; outputs are bit-identical either way (tested). */
+enum { GSR_OPT_BLEND_CULL = 1 };
+int gsr_set_option(gsr_context *ctx, int option, int64_t value);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSR_H */

@@ -1,0 +1,125 @@
+"""CPU: the C-ABI library loads and exports every symbol include/gsr.h declares, its struct
+layouts agree with the ctypes mirrors, and the host-side API validates like upstream."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from gaussiansplattingviewer_amd import _lib
+from gaussiansplattingviewer_amd.rasterizer import (GaussianRasterizationSettings,
+                                                    GaussianRasterizer, rasterize_gaussians_native)
+from gaussiansplattingviewer_amd.strips import strip_rows, strip_pixel_rows
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "gsr.h")
+
+
+def _header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return set(re.findall(r"\b(gsr_[a-z_]+)\s*\(", src))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load_library()
+    declared = _header_functions()
+    assert declared == set(_lib.EXPORTED_SYMBOLS)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.gsr_abi_version() == _lib.ABI_VERSION
+    assert _lib.stage_names() == ["preprocess", "depth_sort", "scan", "duplicate", "tile_sort",
+                                  "ranges", "blend"]
+
+
+def test_library_is_gfx950_code_object():
+    """The embedded device code object targets gfx950 (the MI355X) and nothing else."""
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
+        assert other not in data
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """Compile a probe against include/gsr.h with gcc and compare offsets with ctypes."""
+    probe = tmp_path / "probe.c"
+    fields = {
+        "gsr_gaussians": [f for f, _ in _lib.GsrGaussians._fields_],
+        "gsr_raster_settings": [f for f, _ in _lib.GsrRasterSettings._fields_],
+        "gsr_outputs": [f for f, _ in _lib.GsrOutputs._fields_],
+    }
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "gsr.h"', "int main(void){"]
+    for st, fs in fields.items():
+        lines.append(f'printf("{st} size %zu\\n", sizeof({st}));')
+        for f in fs:
+            lines.append(f'printf("{st} {f} %zu\\n", offsetof({st}, {f}));')
+    lines.append("return 0;}")
+    probe.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(REPO, "include"), str(probe), "-o",
+                    str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l}
+    for st, cls in [("gsr_gaussians", _lib.GsrGaussians),
+                    ("gsr_raster_settings", _lib.GsrRasterSettings),
+                    ("gsr_outputs", _lib.GsrOutputs)]:
+        assert got[(st, "size")] == ctypes.sizeof(cls), st
+        for f, _ in cls._fields_:
+            assert got[(st, f)] == getattr(cls, f).offset, (st, f)
+
+
+def _settings(H=64, W=64):
+    eye = torch.eye(4)
+    return GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=0.5, tanfovy=0.5,
+                                         bg=torch.zeros(3), scale_modifier=1.0, viewmatrix=eye,
+                                         projmatrix=eye, sh_degree=0, campos=torch.zeros(3),
+                                         prefiltered=False, debug=False)
+
+
+def test_rasterizer_argument_checks_match_upstream():
+    r = GaussianRasterizer(_settings())
+    x = torch.zeros(4, 3)
+    with pytest.raises(Exception, match="excatly one of either SHs or precomputed colors"):
+        r(means3D=x, means2D=None, opacities=torch.ones(4, 1), shs=None, colors_precomp=None,
+          scales=torch.ones(4, 3), rotations=torch.ones(4, 4))
+    with pytest.raises(Exception, match="excatly one of either SHs"):
+        r(means3D=x, means2D=None, opacities=torch.ones(4, 1), shs=torch.ones(4, 1, 3),
+          colors_precomp=torch.ones(4, 3), scales=torch.ones(4, 3), rotations=torch.ones(4, 4))
+    with pytest.raises(Exception, match="scale/rotation pair or precomputed 3D covariance"):
+        r(means3D=x, means2D=None, opacities=torch.ones(4, 1), shs=torch.ones(4, 1, 3),
+          scales=torch.ones(4, 3), rotations=None)
+    with pytest.raises(Exception, match="scale/rotation pair or precomputed 3D covariance"):
+        r(means3D=x, means2D=None, opacities=torch.ones(4, 1), shs=torch.ones(4, 1, 3),
+          scales=torch.ones(4, 3), rotations=torch.ones(4, 4), cov3D_precomp=torch.ones(4, 6))
+
+
+def test_native_rejects_bad_means_shape():
+    with pytest.raises(RuntimeError, match=r"means3D must have dimensions \(num_points, 3\)"):
+        rasterize_gaussians_native(torch.zeros(3), torch.zeros(4, 4), None, torch.ones(4, 1),
+                                   None, None, 1.0, None, torch.eye(4), torch.eye(4), 1.0, 1.0,
+                                   8, 8, torch.zeros(4, 1, 3), 0, torch.zeros(3), False, False)
+
+
+def test_no_cpu_fallback():
+    """Host tensors never get rendered on the CPU: the product path refuses them."""
+    with pytest.raises(RuntimeError, match="device"):
+        rasterize_gaussians_native(torch.zeros(3), torch.zeros(4, 3), None, torch.ones(4, 1),
+                                   torch.ones(4, 3), torch.ones(4, 4), 1.0, None, torch.eye(4),
+                                   torch.eye(4), 1.0, 1.0, 8, 8, torch.zeros(4, 1, 3), 0,
+                                   torch.zeros(3), False, False)
+
+
+@pytest.mark.parametrize("gy,world", [(68, 1), (68, 2), (68, 8), (135, 8), (30, 4), (5, 8)])
+def test_strip_rows_partition(gy, world):
+    rows = [strip_rows(gy, world, r) for r in range(world)]
+    assert rows[0][0] == 0 and rows[-1][1] == gy
+    for (a0, a1), (b0, b1) in zip(rows, rows[1:]):
+        assert a1 == b0
+    sizes = [b - a for a, b in rows]
+    assert max(sizes) - min(sizes) <= 1
+    H = gy * 16 - 7
+    covered = sum(strip_pixel_rows(r, H)[1] for r in rows)
+    assert covered == H

@@ -1,0 +1,167 @@
+"""GPU parity: the HIP rasterizer (libgsr.so through its C ABI) against the CPU oracle.
+
+Bit-exact: radii, tiles_touched, depths, means2D, conic_opacity, rgb, num_rendered, the
+sorted point list, its tile ids, and the tile ranges.  Image (color, final_T, n_contrib): the
+tolerance in gpu_helpers.py (expf is the only non-bit-exact operation)."""
+import numpy as np
+import pytest
+import torch
+
+from gaussiansplattingviewer_amd import _lib
+from gaussiansplattingviewer_amd.camera import Camera, static_camera
+from gaussiansplattingviewer_amd.gaussian_data import (GaussianData, naive_gaussian,
+                                                       synthetic_gaussians)
+
+from gpu_helpers import (assert_image_close, assert_parity, run_hip, run_oracle, scene_inputs)
+
+pytestmark = pytest.mark.gpu
+
+
+def _set_cull(dev, on):
+    lib = _lib.load_library()
+    _lib.check(lib.gsr_set_option(_lib.context(dev.index or 0), _lib.GSR_OPT_BLEND_CULL, int(on)),
+               "gsr_set_option")
+
+
+CASES = {
+    # name: (P, W, H, sh_degree, seed, eye)
+    "C1_10k_640x480_sh3": (10_000, 640, 480, 3, 0, (0.0, 0.0, 4.0)),
+    "C2_100k_1080p_sh0": (100_000, 1920, 1080, 0, 1, (0.0, 0.0, 4.0)),
+    "oblique_30k_800x600_sh3": (30_000, 800, 600, 3, 4, (2.5, 1.0, -3.0)),
+    "inside_cloud_20k_1160x522_sh3": (20_000, 1160, 522, 3, 5, (0.3, -0.2, 0.5)),
+}
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_forward_parity(gpu, oracle_mod, name):
+    P, W, H, deg, seed, eye = CASES[name]
+    s = scene_inputs(synthetic_gaussians(P, deg, seed), static_camera(W, H, eye), deg)
+    orc = run_oracle(oracle_mod, s)
+    hip = run_hip(s, gpu)
+    assert orc["num_rendered"] > 0
+    assert_parity(hip, orc)
+
+
+def test_naive_scene_viewer_window(gpu, oracle_mod):
+    """The viewer's default 4-Gaussian scene (util_gau.py:25-60) in its 1160x522 window."""
+    cam = Camera(522, 1160)
+    cam.look_from((0.4, 0.3, 3.0))
+    s = scene_inputs(naive_gaussian(), cam, 0)
+    assert_parity(run_hip(s, gpu), run_oracle(oracle_mod, s))
+
+
+@pytest.mark.parametrize("deg", [1, 2])
+def test_lower_sh_degree_with_degree3_storage(gpu, oracle_mod, deg):
+    s = scene_inputs(synthetic_gaussians(8000, 3, 12), static_camera(512, 384), deg)
+    assert_parity(run_hip(s, gpu), run_oracle(oracle_mod, s))
+
+
+def test_background_and_scale_modifier(gpu, oracle_mod):
+    s = scene_inputs(synthetic_gaussians(15_000, 3, 13), static_camera(700, 500, (1, 1, 3.5)), 3,
+                     bg=(0.25, 0.5, 1.0), scale_modifier=1.7)
+    assert_parity(run_hip(s, gpu), run_oracle(oracle_mod, s))
+
+
+def test_precomputed_colors_and_covariance(gpu, oracle_mod):
+    g = synthetic_gaussians(6000, 0, 14)
+    rng = np.random.default_rng(14)
+    colors = rng.uniform(0, 1, (len(g), 3)).astype(np.float32)
+    A = rng.normal(0, 0.03, (len(g), 3, 3))
+    cov = np.einsum("pij,pkj->pik", A, A)
+    cov6 = np.stack([cov[:, 0, 0], cov[:, 0, 1], cov[:, 0, 2], cov[:, 1, 1], cov[:, 1, 2],
+                     cov[:, 2, 2]], -1).astype(np.float32)
+    s = scene_inputs(g, static_camera(480, 360), 0)
+    orc = run_oracle(oracle_mod, s, colors_precomp=colors, cov3D_precomp=cov6)
+    hip = run_hip(s, gpu, colors_precomp=colors, cov3D_precomp=cov6)
+    orc["rgb"] = np.zeros_like(orc["rgb"])  # not computed on either side with precomp colors
+    assert_parity(hip, orc)
+
+
+def test_large_splats_many_tiles(gpu, oracle_mod):
+    """A few huge Gaussians close to the camera: each touches most of the frame's tiles."""
+    g = synthetic_gaussians(300, 3, 15)
+    g.scale[:] = np.float32(0.4)
+    s = scene_inputs(g, static_camera(640, 480, (0, 0, 2.2)), 3)
+    orc = run_oracle(oracle_mod, s)
+    assert orc["num_rendered"] > 300 * 100
+    assert_parity(run_hip(s, gpu), orc)
+
+
+def test_empty_and_fully_culled(gpu, oracle_mod):
+    # P = 0: upstream returns a zero image (not the background)
+    empty = GaussianData(*(np.zeros((0, k), np.float32) for k in (3, 4, 3, 1, 3)))
+    s = scene_inputs(empty, static_camera(64, 48), 0, bg=(0.3, 0.3, 0.3))
+    hip = run_hip(s, gpu, extras=(), binning=False)
+    assert hip["num_rendered"] == 0 and hip["radii"].shape == (0,)
+    assert np.all(hip["color"] == 0)
+    # everything behind the camera: no pairs, background everywhere
+    g = synthetic_gaussians(1000, 0, 16)
+    g.xyz[:, 2] = g.xyz[:, 2] + 10.0
+    s = scene_inputs(g, static_camera(100, 70), 0, bg=(0.1, 0.2, 0.3))
+    orc = run_oracle(oracle_mod, s)
+    hip = run_hip(s, gpu)
+    assert orc["num_rendered"] == 0
+    assert_parity(hip, orc)
+    assert np.all(hip["color"][1] == np.float32(0.2))
+
+
+def test_cull_is_exact(gpu, oracle_mod):
+    """The blend's per-wave ellipse cull changes nothing: bit-identical image either way."""
+    s = scene_inputs(synthetic_gaussians(200_000, 3, 17), static_camera(1280, 720), 3)
+    _set_cull(gpu, False)
+    try:
+        off = run_hip(s, gpu, binning=False)
+    finally:
+        _set_cull(gpu, True)
+    on = run_hip(s, gpu, binning=False)
+    for k in ("color", "final_T", "n_contrib"):
+        np.testing.assert_array_equal(on[k].view(np.uint32), off[k].view(np.uint32), err_msg=k)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_strips_equal_full_frame_rows(gpu, world):
+    """Each strip of the multi-GPU partition is bit-identical to the same rows of the 1-GPU
+    frame (here rendered one strip after another on one device)."""
+    from gaussiansplattingviewer_amd.strips import strip_pixel_rows, strip_rows
+    W, H = 1920, 1080
+    s = scene_inputs(synthetic_gaussians(150_000, 3, 18), static_camera(W, H), 3)
+    full = run_hip(s, gpu)
+    gy = (H + 15) // 16
+    K_sum = 0
+    for r in range(world):
+        rows = strip_rows(gy, world, r)
+        part = run_hip(s, gpu, tile_rows=rows)
+        y0, n = strip_pixel_rows(rows, H)
+        np.testing.assert_array_equal(part["color"].view(np.uint32),
+                                      full["color"][:, y0:y0 + n].view(np.uint32))
+        np.testing.assert_array_equal(part["n_contrib"], full["n_contrib"][y0:y0 + n])
+        np.testing.assert_array_equal(part["radii"], full["radii"])
+        t0, t1 = rows[0] * 120, rows[1] * 120
+        before = int((full["point_tiles"] < t0).sum())
+        nonempty = full["ranges"][t0:t1, 1] > full["ranges"][t0:t1, 0]
+        np.testing.assert_array_equal(part["ranges"][t0:t1][nonempty],
+                                      full["ranges"][t0:t1][nonempty] - before)
+        assert np.all(part["ranges"][t0:t1][~nonempty] == 0)
+        assert np.all(part["ranges"][:t0] == 0) and np.all(part["ranges"][t1:] == 0)
+        sel = (full["point_tiles"] >= t0) & (full["point_tiles"] < t1)
+        np.testing.assert_array_equal(part["point_list"], full["point_list"][sel])
+        np.testing.assert_array_equal(part["point_tiles"], full["point_tiles"][sel])
+        K_sum += part["num_rendered"]
+    assert K_sum == full["num_rendered"]
+
+
+def test_debug_mode_and_repeatability(gpu):
+    s = scene_inputs(synthetic_gaussians(50_000, 3, 19), static_camera(960, 540), 3)
+    a = run_hip(s, gpu, debug=True)
+    b = run_hip(s, gpu)
+    for k in ("color", "point_list", "ranges", "radii"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_headline_config_c3(gpu, oracle_mod):
+    """Config C3 at full size: 1M Gaussians, 1920x1080, SH degree 3, static camera."""
+    s = scene_inputs(synthetic_gaussians(1_000_000, 3, 2), static_camera(1920, 1080), 3)
+    orc = run_oracle(oracle_mod, s)
+    hip = run_hip(s, gpu)
+    assert orc["num_rendered"] > 5_000_000
+    assert_parity(hip, orc)

@@ -1,0 +1,66 @@
+"""GPU: the device depth-sort backend (replacing renderer_ogl.py:10-53) against the reference's
+own outputs (tests/golden/sort_backend.npz) and stable-sort properties at full size."""
+import numpy as np
+import pytest
+import torch
+
+from gaussiansplattingviewer_amd.camera import look_at
+from gaussiansplattingviewer_amd.renderer import _sort_gaussian_hip, depth_argsort
+
+pytestmark = pytest.mark.gpu
+
+CASES = ["10k_front", "10k_oblique", "10k_viewer_default", "100k_front", "ties_front"]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_depth_bits_and_order_vs_reference(gpu, golden, case):
+    g = golden("sort_backend.npz")
+    xyz = g["xyz_" + case.split("_")[0]]
+    view = g[case + "__view"]
+    ref_depth = g[case + "__depth"]
+    ref_idx = g[case + "__index"][:, 0]
+    idx, depth = depth_argsort(torch.as_tensor(xyz).to(gpu), view, return_depth=True)
+    idx, depth = idx.cpu().numpy(), depth.cpu().numpy()
+    # depth: bit-exact with the array the reference sorted
+    np.testing.assert_array_equal(depth.view(np.uint32), ref_depth.view(np.uint32))
+    # order: exactly numpy's stable argsort; same sorted sequence as the reference's unstable one
+    np.testing.assert_array_equal(idx, np.argsort(ref_depth, kind="stable"))
+    np.testing.assert_array_equal(ref_depth[idx], ref_depth[ref_idx])
+
+
+def test_sort_backend_contract(gpu, golden):
+    g = golden("sort_backend.npz")
+    gaus = type("G", (), {})()
+    gaus.xyz = g["xyz_10k"]
+    out = _sort_gaussian_hip(gaus, g["10k_front__view"])
+    assert isinstance(out, np.ndarray) and out.dtype == np.int32 and out.shape == (10_000, 1)
+    ref = g["10k_front__index"]
+    d = g["10k_front__depth"]
+    np.testing.assert_array_equal(d[out[:, 0]], d[ref[:, 0]])
+
+
+@pytest.mark.parametrize("P", [1, 2, 4095, 4096, 4097, 1_000_000, 6_000_000])
+def test_stable_permutation_full_size(gpu, P):
+    rng = np.random.default_rng(P)
+    xyz = rng.standard_normal((P, 3)).astype(np.float32)
+    xyz[::7] = np.round(xyz[::7] * 8) / 8  # inject ties
+    xyz[::11, 2] = -0.0
+    view = look_at((0.3, 0.1, 4.0), (0, 0, 0), (0, 1, 0))
+    idx, depth = depth_argsort(torch.as_tensor(xyz).to(gpu), view, return_depth=True)
+    idx, depth = idx.cpu().numpy(), depth.cpu().numpy()
+    assert np.array_equal(np.sort(idx), np.arange(P))          # a permutation
+    ds = depth[idx]
+    assert np.all(ds[1:] >= ds[:-1])                           # ascending
+    tie = ds[1:] == ds[:-1]
+    assert np.all(idx[1:][tie] > idx[:-1][tie])                # stable among ties
+    if P <= 1_000_000:
+        np.testing.assert_array_equal(idx, np.argsort(depth, kind="stable"))
+
+
+def test_negative_nan_and_signed_zero_keys(gpu):
+    xyz = np.array([[0, 0, 1], [0, 0, -1], [0, 0, 0], [0, 0, -0.0], [0, 0, np.nan],
+                    [0, 0, 2], [0, 0, -3], [0, 0, np.inf], [0, 0, -np.inf]], np.float32)
+    view = np.eye(4, dtype=np.float32)
+    idx, depth = depth_argsort(torch.as_tensor(xyz).to(gpu), view, return_depth=True)
+    d = depth.cpu().numpy()
+    np.testing.assert_array_equal(idx.cpu().numpy(), np.argsort(d, kind="stable"))
