@@ -16,8 +16,8 @@ using namespace gsr;
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kItems = 16;
-constexpr int kTile = kBlock * kItems;  // 4096 depth-sorted Gaussians per block
+constexpr int kItems = 4;
+constexpr int kTile = kBlock * kItems;  // 1024 depth-sorted Gaussians per block
 
 // Pass 1 of the scan: per-block sum of the strip tile counts, gathered in depth order.
 __global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t *__restrict__ perm,
@@ -53,17 +53,24 @@ __global__ __launch_bounds__(kBlock) void k_scan_partials(uint32_t *__restrict__
     if (threadIdx.x == 0) *total = carry;
 }
 
-// Pass 3 fused with upstream duplicateWithKeys: block scan of the tile counts of 4096
-// depth-sorted Gaussians (blocked: thread t owns elements 16t..16t+15), then every Gaussian
-// writes one (strip-local tile id, Gaussian id) pair per tile of its rect inside the strip,
-// row-major like upstream.
+// Pass 3 fused with upstream duplicateWithKeys: block scan of the strip tile counts of 1024
+// depth-sorted Gaussians (blocked: thread t owns elements 4t..4t+3), then the block expands
+// them into (strip-local tile id, Gaussian id) pairs, row-major over each rect like upstream.
+// The expansion is output-driven so the stores are coalesced: thread i of the block writes
+// pairs i, i+256, ... of the block's contiguous output range and finds the Gaussian that owns
+// pair i by binary search over the block-local inclusive ends in LDS.
 __global__ __launch_bounds__(kBlock) void k_duplicate(
     const uint32_t *__restrict__ perm, const uint32_t *__restrict__ strip_tiles,
     const uint32_t *__restrict__ partials, int64_t n, const SplatRecord *__restrict__ records,
     uint32_t gx, uint32_t gy, uint32_t row_begin, uint32_t row_end, uint32_t *__restrict__ tile_keys,
     uint32_t *__restrict__ tile_vals) {
+    __shared__ uint32_t s_end[kTile];  // inclusive end of each element's pairs (block-local)
+    __shared__ uint32_t s_id[kTile];
+    __shared__ uint32_t s_x0w[kTile];  // rect x0 | width << 16
+    __shared__ uint32_t s_row0[kTile]; // first strip-local tile row * gx
     __shared__ uint32_t s_tmp[4];
-    const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kItems;
+    const int tid = threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)tid * kItems;
     uint32_t id[kItems], cnt[kItems], sum = 0;
 #pragma unroll
     for (int j = 0; j < kItems; ++j) {
@@ -73,23 +80,41 @@ __global__ __launch_bounds__(kBlock) void k_duplicate(
         sum += cnt[j];
     }
     uint32_t total;
-    uint32_t off = block256_exclusive_scan(sum, s_tmp, total) + partials[blockIdx.x];
+    uint32_t off = block256_exclusive_scan(sum, s_tmp, total);
 #pragma unroll
     for (int j = 0; j < kItems; ++j) {
-        if (cnt[j] == 0) continue;
-        const SplatRecord &r = records[id[j]];
-        const float4 a = r.a;
-        const int radius = __float_as_int(r.c.w);
-        const Rect rc = get_rect(a.x, a.y, radius, gx, gy);
-        const uint32_t y0 = max(rc.y0, row_begin), y1 = min(rc.y1, row_end);
-        for (uint32_t y = y0; y < y1; ++y) {
-            const uint32_t row = (y - row_begin) * gx;
-            for (uint32_t x = rc.x0; x < rc.x1; ++x) {
-                tile_keys[off] = row + x;
-                tile_vals[off] = id[j];
-                ++off;
-            }
+        const int le = tid * kItems + j;
+        uint32_t x0w = 0, row0 = 0;
+        if (cnt[j]) {
+            const SplatRecord &r = records[id[j]];
+            const float4 ra = r.a;
+            const Rect rc = get_rect(ra.x, ra.y, __float_as_int(r.c.w), gx, gy);
+            x0w = rc.x0 | ((rc.x1 - rc.x0) << 16);
+            row0 = (max(rc.y0, row_begin) - row_begin) * gx;
         }
+        off += cnt[j];
+        s_end[le] = off;
+        s_id[le] = id[j];
+        s_x0w[le] = x0w;
+        s_row0[le] = row0;
+    }
+    __syncthreads();
+    const uint32_t gbase = partials[blockIdx.x];
+    for (uint32_t i = tid; i < total; i += kBlock) {
+        int lo = 0, hi = kTile - 1;  // first element whose inclusive end exceeds i
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_end[mid] > i) hi = mid;
+            else lo = mid + 1;
+        }
+        const uint32_t first = lo > 0 ? s_end[lo - 1] : 0u;
+        const uint32_t local = i - first;
+        const uint32_t x0w = s_x0w[lo];
+        const uint32_t width = x0w >> 16;
+        const uint32_t row = local / width;
+        const uint32_t col = local - row * width;
+        tile_keys[gbase + i] = s_row0[lo] + row * gx + (x0w & 0xFFFFu) + col;
+        tile_vals[gbase + i] = s_id[lo];
     }
 }
 

@@ -2,16 +2,23 @@
 //
 // Replaces upstream diff-gaussian-rasterization forward.cu renderCUDA (GLSL twin of the
 // per-pixel alpha: shaders/gau_frag.glsl:21-27).  One 256-thread block per 16x16 tile; each
-// of its 4 waves owns an 8x8 quadrant (one pixel per lane).  The tile's depth-sorted splat
-// list is staged through LDS 256 records (12 KB) at a time; `__syncthreads_count(done)`
-// ends the tile when every pixel has saturated (as upstream).  Per splat each wave first
-// tests the splat's conservative alpha>=1/255 box against its quadrant and skips the splat
-// as a whole (wave-uniform branch) when they do not overlap; otherwise every lane runs the
-// upstream per-pixel arithmetic verbatim (same operation order, accurate expf).
+// of its 4 waves owns an 8x8 quadrant, one pixel per lane.  The tile's depth-sorted splat list
+// is staged through LDS 256 splats at a time; `__syncthreads_count(done)` ends the tile when
+// every pixel has saturated, as upstream.
 //
-// n_contrib equals upstream's running `contributor` counter at the last contributing splat
-// = (position of that splat in the tile list) + 1, so skipping non-contributing splats does
-// not change it.
+// gfx950-specific structure:
+//  * cull once per staged splat, not once per (splat, wave): the loading thread tests the
+//    splat's conservative alpha >= 1/255 box against the tile's four quadrants and stores a
+//    4-bit mask; each wave then compacts the batch to the splats that can touch its quadrant
+//    (ballot + popcount) and loops over that list only;
+//  * branch-free per-pixel body (selects instead of nested ifs, so no exec-mask churn) with
+//    the LDS reads of the next splat issued before the current one is evaluated;
+//  * exp: the core of ocml's expf (range-reduced v_exp_f32 + ldexp), bit-identical to expf
+//    over the range that matters, without its under/overflow selects.
+// The per-pixel arithmetic keeps upstream's operation order, so the image differs from the
+// CPU oracle only through expf itself (device vs glibc).  n_contrib equals upstream's running
+// `contributor` at the last contributing splat = its position in the tile list + 1, so
+// skipping splats that cannot contribute does not change it.
 #include "gsr_internal.h"
 
 using namespace gsr;
@@ -20,22 +27,34 @@ namespace {
 
 constexpr int kBatch = 256;
 
+// ocml __ocml_exp_f32 (non-DAZ path) without the final range selects: identical results for
+// every finite argument (below about -104 both give 0, above 88.7 both give +inf).
+__device__ __forceinline__ float exp_core(float x) {
+    const float kLog2eHi = 0x1.715476p+0f;   // 1.44269502
+    const float kLog2eLo = 0x1.4ae0bep-26f;  // 1.92596299e-08
+    const float ph = x * kLog2eHi;
+    const float n = __builtin_rintf(ph);
+    const float hi = ph - n;
+    float lo = __builtin_fmaf(x, kLog2eHi, -ph);
+    lo = __builtin_fmaf(x, kLog2eLo, lo);
+    const float e = __builtin_amdgcn_exp2f(hi + lo);
+    return __builtin_ldexpf(e, (int)n);
+}
+
 __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
-    __shared__ float4 s_a[kBatch];
-    __shared__ float4 s_b[kBatch];
-    __shared__ float4 s_c[kBatch];
+    __shared__ float4 s_geo[kBatch];   // x, y, conic.a, conic.b
+    __shared__ float4 s_opc[kBatch];   // conic.c, opacity, r, g
+    __shared__ float s_blue[kBatch];   // b
+    __shared__ uint8_t s_mask[kBatch]; // quadrant bits of each staged splat
+    __shared__ uint8_t s_list[4][kBatch];
 
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t tx = blockIdx.x, ty_local = blockIdx.y, ty = a.row_begin + ty_local;
-    const int qx0 = (int)tx * GSR_TILE_X + (w & 1) * 8;
-    const int qy0 = (int)ty * GSR_TILE_Y + (w >> 1) * 8;
-    const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
+    const int tx0 = (int)tx * GSR_TILE_X, ty0 = (int)ty * GSR_TILE_Y;
+    const int px = tx0 + (w & 1) * 8 + (lane & 7), py = ty0 + (w >> 1) * 8 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
     bool done = !inside;
     const float pfx = (float)px, pfy = (float)py;
-    // quadrant bounds (pixel centres are the integer coordinates, upstream has no +0.5)
-    const float qxlo = (float)qx0, qxhi = (float)(qx0 + 7);
-    const float qylo = (float)qy0, qyhi = (float)(qy0 + 7);
 
     const uint2 range = a.ranges[ty_local * a.grid_x + tx];
     float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
@@ -45,48 +64,70 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
         if (__syncthreads_count(done) == 256) break;
         const uint32_t idx = start + tid;
         if (idx < range.y) {
-            const SplatRecord *r = a.records + a.point_list[idx];
-            s_a[tid] = r->a;
-            s_b[tid] = r->b;
-            s_c[tid] = r->c;
+            const SplatRecord r = a.records[a.point_list[idx]];
+            s_geo[tid] = r.a;
+            s_opc[tid] = r.b;
+            s_blue[tid] = r.c.x;
+            uint32_t m = 0xF;
+            if (a.cull) {
+                // distance from the splat centre to each 8x8 quadrant, along x and y
+                const float x = r.a.x, y = r.a.y, ex = r.c.y, ey = r.c.z;
+                const float lx0 = (float)tx0, hx0 = (float)(tx0 + 7);
+                const float lx1 = (float)(tx0 + 8), hx1 = (float)(tx0 + 15);
+                const float ly0 = (float)ty0, hy0 = (float)(ty0 + 7);
+                const float ly1 = (float)(ty0 + 8), hy1 = (float)(ty0 + 15);
+                const bool inx0 = !(fmaxf(fmaxf(lx0 - x, x - hx0), 0.0f) > ex);
+                const bool inx1 = !(fmaxf(fmaxf(lx1 - x, x - hx1), 0.0f) > ex);
+                const bool iny0 = !(fmaxf(fmaxf(ly0 - y, y - hy0), 0.0f) > ey);
+                const bool iny1 = !(fmaxf(fmaxf(ly1 - y, y - hy1), 0.0f) > ey);
+                m = (uint32_t)(inx0 && iny0) | ((uint32_t)(inx1 && iny0) << 1) |
+                    ((uint32_t)(inx0 && iny1) << 2) | ((uint32_t)(inx1 && iny1) << 3);
+            }
+            s_mask[tid] = (uint8_t)m;
         }
         __syncthreads();
         const int n = (int)min((uint32_t)kBatch, range.y - start);
-        if (__ballot(!done) != 0ull) {
-            for (int j = 0; j < n; ++j) {
-                const float4 sa = s_a[j];
-                if (a.cull) {
-                    const float4 sc = s_c[j];
-                    // distance from the splat centre to the quadrant along x and y
-                    const float ddx = fmaxf(fmaxf(qxlo - sa.x, sa.x - qxhi), 0.0f);
-                    const float ddy = fmaxf(fmaxf(qylo - sa.y, sa.y - qyhi), 0.0f);
-                    const bool miss = (ddx > sc.y) || (ddy > sc.z);
-                    if (__builtin_amdgcn_readfirstlane((int)miss)) continue;
-                }
-                if (!done) {
-                    const float4 sb = s_b[j];
-                    const float dx = sa.x - pfx, dy = sa.y - pfy;
-                    const float power =
-                        -0.5f * (sa.z * dx * dx + sb.x * dy * dy) - sa.w * dx * dy;
-                    if (!(power > 0.0f)) {  // upstream: if (power > 0) continue;
-                        const float alpha = fminf(0.99f, sb.y * expf(power));
-                        if (!(alpha < 1.0f / 255.0f)) {
-                            const float test_T = T * (1 - alpha);
-                            if (test_T < 0.0001f) {
-                                done = true;
-                            } else {
-                                const float cz = s_c[j].x;
-                                C0 += sb.z * alpha * T;
-                                C1 += sb.w * alpha * T;
-                                C2 += cz * alpha * T;
-                                T = test_T;
-                                last_contributor = start - range.x + (uint32_t)j + 1u;
-                            }
-                        }
-                    }
-                }
-                if (__ballot(!done) == 0ull) break;
-            }
+
+        // This wave's splats of the batch, in list order.
+        int count = 0;
+        for (int base = 0; base < n; base += 64) {
+            const int j = base + lane;
+            const bool keep = j < n && ((s_mask[j] >> w) & 1u);
+            const uint64_t bal = __ballot(keep);
+            const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+            if (keep) s_list[w][count + __popcll(bal & lt)] = (uint8_t)j;
+            count += __popcll(bal);
+        }
+        // s_list[w] is written and read by this wave only: LDS ops of one wave execute in
+        // order, so no barrier is needed before the reads below.
+        if (count == 0 || __ballot(!done) == 0ull) continue;
+
+        int j = s_list[w][0];
+        float4 g = s_geo[j], q = s_opc[j];
+        float blue = s_blue[j];
+        for (int k = 0; k < count; ++k) {
+            const int jn = s_list[w][k + 1 < count ? k + 1 : k];
+            const float4 g_next = s_geo[jn], q_next = s_opc[jn];
+            const float blue_next = s_blue[jn];
+            // upstream renderCUDA per-pixel body, same operation order
+            const float dx = g.x - pfx, dy = g.y - pfy;
+            const float power = -0.5f * (g.z * dx * dx + q.x * dy * dy) - g.w * dx * dy;
+            const float alpha = fminf(0.99f, q.y * exp_core(power));
+            const float test_T = T * (1 - alpha);
+            const bool live = !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+            const bool term = live && (test_T < 0.0001f);
+            const bool acc = live && !(test_T < 0.0001f);
+            C0 = acc ? C0 + q.z * alpha * T : C0;
+            C1 = acc ? C1 + q.w * alpha * T : C1;
+            C2 = acc ? C2 + blue * alpha * T : C2;
+            T = acc ? test_T : T;
+            last_contributor = acc ? start - range.x + (uint32_t)j + 1u : last_contributor;
+            done = done || term;
+            j = jn;
+            g = g_next;
+            q = q_next;
+            blue = blue_next;
+            if ((k & 15) == 15 && __ballot(!done) == 0ull) break;
         }
     }
 

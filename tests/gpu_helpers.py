@@ -35,7 +35,7 @@ def run_hip(s, dev, tile_rows=None, colors_precomp=None, cov3D_precomp=None, ext
             binning=True, debug=False):
     g = s["g"]
     P = len(g.xyz)
-    sh = None if colors_precomp is not None else to_dev(g.sh.reshape(P, -1, 3), dev)
+    sh = None if colors_precomp is not None else to_dev(g.sh.reshape(P, g.sh.shape[-1] // 3, 3), dev)
     use_sr = cov3D_precomp is None
     res = rasterize_gaussians_native(
         to_dev(s["bg"], dev), to_dev(g.xyz, dev), to_dev(colors_precomp, dev),

@@ -1,0 +1,82 @@
+"""Summarise a tools/profile.sh run: per-kernel average duration (rocprofv3 kernel trace) and
+HBM traffic per launch from the FETCH_SIZE / WRITE_SIZE passes.
+
+FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE counts exactly half of the bytes of
+a wide coalesced streaming read (MI355X_MICROARCH.md §HBM), so the table shows the raw read
+bytes and the x2-corrected read bytes; WRITE_SIZE is exact for 16-B streaming stores.
+
+Usage: python tools/prof_summary.py gpurun_out/prof_<tag> [--out profiles/<name>.md]
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import os
+import re
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    m = re.search(r"::(k_[a-z0-9_]+)", name)
+    if m:
+        return m.group(1)
+    return name.split("(")[0][:60]
+
+
+def load_stats(d):
+    path = os.path.join(d, "trace", "trace_kernel_stats.csv")
+    rows = list(csv.DictReader(open(path)))
+    return {short(r["Name"]): (int(r["Calls"]), float(r["AverageNs"]), float(r["TotalDurationNs"]))
+            for r in rows}
+
+
+def load_trace(d):
+    path = os.path.join(d, "trace", "trace_kernel_trace.csv")
+    per = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        per[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return per
+
+
+def load_pmc(d, counter):
+    path = os.path.join(d, f"pmc_{counter}", "pmc_counter_collection.csv")
+    if not os.path.exists(path):
+        return {}
+    per = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            per[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    return per
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--out")
+    ap.add_argument("--title", default="")
+    a = ap.parse_args()
+    stats = load_stats(a.dir)
+    fetch = load_pmc(a.dir, "FETCH_SIZE")
+    write = load_pmc(a.dir, "WRITE_SIZE")
+    total = sum(v[2] for v in stats.values())
+    lines = [f"# rocprofv3 summary {a.title}".rstrip(), "",
+             f"Source: `{a.dir}` (kernel trace + stats; FETCH_SIZE and WRITE_SIZE in separate "
+             "passes).", "",
+             "| kernel | calls | avg us | share | FETCH MB/launch (raw) | read MB x2-corr | "
+             "WRITE MB/launch |", "|---|---|---|---|---|---|---|"]
+    for k, (calls, avg, tot) in sorted(stats.items(), key=lambda kv: -kv[1][2]):
+        f = fetch.get(k)
+        w = write.get(k)
+        fmb = sum(f) / len(f) * 1024 / 1e6 if f else float("nan")
+        wmb = sum(w) / len(w) * 1024 / 1e6 if w else float("nan")
+        lines.append(f"| {k} | {calls} | {avg / 1e3:.2f} | {100 * tot / total:.1f}% | {fmb:.2f} | "
+                     f"{2 * fmb:.2f} | {wmb:.2f} |")
+    text = "\n".join(lines) + "\n"
+    print(text)
+    if a.out:
+        os.makedirs(os.path.dirname(a.out), exist_ok=True)
+        open(a.out, "w").write(text)
+
+
+if __name__ == "__main__":
+    main()
