@@ -43,7 +43,7 @@ struct gsr_context {
     int device = 0;
     // per-Gaussian workspace
     DevBuf records, strip_tiles, sort_keys, sort_vals, sort_keys_alt, sort_vals_alt, partials,
-        total, hist, digit_total;
+        total, hist, digit_total, offsets, chunk_first;
     // per-pair workspace
     DevBuf tile_keys, tile_vals, tile_keys_alt, tile_vals_alt;
     DevBuf ranges_local;
@@ -103,6 +103,7 @@ int reserve_P(gsr_context *ctx, int64_t P, hipStream_t s) {
     GSR_TRY(grow(ctx, ctx->total, 16, s));
     GSR_TRY(grow(ctx, ctx->hist, (size_t)gsr_radix_hist_words(P) * 4, s));
     GSR_TRY(grow(ctx, ctx->digit_total, 256 * 4, s));
+    GSR_TRY(grow(ctx, ctx->offsets, n * 4, s));
     return GSR_OK;
 }
 
@@ -113,6 +114,7 @@ int reserve_K(gsr_context *ctx, int64_t K, hipStream_t s) {
     GSR_TRY(grow(ctx, ctx->tile_keys_alt, n * 4, s));
     GSR_TRY(grow(ctx, ctx->tile_vals_alt, n * 4, s));
     GSR_TRY(grow(ctx, ctx->hist, (size_t)gsr_radix_hist_words(K) * 4, s));
+    GSR_TRY(grow(ctx, ctx->chunk_first, (size_t)(gsr_duplicate_chunks(K) + 1) * 4, s));
     return GSR_OK;
 }
 
@@ -162,7 +164,8 @@ void gsr_destroy(gsr_context *ctx) {
     DevBuf *bufs[] = {&ctx->records,       &ctx->strip_tiles,   &ctx->sort_keys,
                       &ctx->sort_vals,     &ctx->sort_keys_alt, &ctx->sort_vals_alt,
                       &ctx->partials,      &ctx->total,         &ctx->hist,
-                      &ctx->digit_total,   &ctx->tile_keys,     &ctx->tile_vals,
+                      &ctx->digit_total,   &ctx->offsets,       &ctx->chunk_first,
+                      &ctx->tile_keys,     &ctx->tile_vals,
                       &ctx->tile_keys_alt, &ctx->tile_vals_alt, &ctx->ranges_local};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
@@ -360,19 +363,26 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     GSR_TRY(stage_end(2));
     GSR_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(num_rendered)");
     const uint64_t K = *ctx->h_total;
-    if (K > (uint64_t)UINT32_MAX)
-        return fail(GSR_E_INVALID, "gsr_forward: more than 2^32-1 (Gaussian, tile) pairs");
+    if (K > (uint64_t)UINT32_MAX - 4096)
+        return fail(GSR_E_INVALID, "gsr_forward: more than 2^32-4097 (Gaussian, tile) pairs");
     GSR_TRY(reserve_K(ctx, (int64_t)K, s));
 
-    // ---- 4. duplicate into (tile, Gaussian) pairs, depth order -------------------------------
+    // ---- 4. duplicate into (tile, Gaussian) pairs, depth order, load-balanced by output ------
     uint32_t *tk = static_cast<uint32_t *>(ctx->tile_keys.p);
     uint32_t *tv = static_cast<uint32_t *>(ctx->tile_vals.p);
     uint32_t *tk_alt = static_cast<uint32_t *>(ctx->tile_keys_alt.p);
     uint32_t *tv_alt = static_cast<uint32_t *>(ctx->tile_vals_alt.p);
+    uint32_t *offsets = static_cast<uint32_t *>(ctx->offsets.p);
+    uint32_t *chunk_first = static_cast<uint32_t *>(ctx->chunk_first.p);
     hist = static_cast<uint32_t *>(ctx->hist.p);  // may have been regrown
-    GSR_HIP(gsr_launch_duplicate(perm, pa.strip_tiles, partials, P, pa.records, gx, gy, rb, re, tk,
-                                 tv, s),
-            "duplicate launch");
+    if (K > 0) {
+        GSR_HIP(gsr_launch_scan_down(perm, pa.strip_tiles, partials, P, d_total, offsets,
+                                     chunk_first, s),
+                "scan_down launch");
+        GSR_HIP(gsr_launch_duplicate(perm, offsets, chunk_first, (int64_t)K, pa.records, gx, gy,
+                                     rb, tk, tv, s),
+                "duplicate launch");
+    }
     GSR_TRY(stage_end(3));
 
     // ---- 5. stable radix sort of the pairs by (strip-local) tile id -------------------------

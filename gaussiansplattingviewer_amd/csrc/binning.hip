@@ -17,7 +17,8 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kItems = 4;
-constexpr int kTile = kBlock * kItems;  // 1024 depth-sorted Gaussians per block
+constexpr int kTile = kBlock * kItems;  // 1024 depth-sorted Gaussians per scan block
+constexpr uint32_t kChunk = 2048;        // output pairs per duplicate block
 
 // Pass 1 of the scan: per-block sum of the strip tile counts, gathered in depth order.
 __global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t *__restrict__ perm,
@@ -53,68 +54,89 @@ __global__ __launch_bounds__(kBlock) void k_scan_partials(uint32_t *__restrict__
     if (threadIdx.x == 0) *total = carry;
 }
 
-// Pass 3 fused with upstream duplicateWithKeys: block scan of the strip tile counts of 1024
-// depth-sorted Gaussians (blocked: thread t owns elements 4t..4t+3), then the block expands
-// them into (strip-local tile id, Gaussian id) pairs, row-major over each rect like upstream.
-// The expansion is output-driven so the stores are coalesced: thread i of the block writes
-// pairs i, i+256, ... of the block's contiguous output range and finds the Gaussian that owns
-// pair i by binary search over the block-local inclusive ends in LDS.
-__global__ __launch_bounds__(kBlock) void k_duplicate(
-    const uint32_t *__restrict__ perm, const uint32_t *__restrict__ strip_tiles,
-    const uint32_t *__restrict__ partials, int64_t n, const SplatRecord *__restrict__ records,
-    uint32_t gx, uint32_t gy, uint32_t row_begin, uint32_t row_end, uint32_t *__restrict__ tile_keys,
-    uint32_t *__restrict__ tile_vals) {
-    __shared__ uint32_t s_end[kTile];  // inclusive end of each element's pairs (block-local)
-    __shared__ uint32_t s_id[kTile];
-    __shared__ uint32_t s_x0w[kTile];  // rect x0 | width << 16
-    __shared__ uint32_t s_row0[kTile]; // first strip-local tile row * gx
+// Pass 3: exclusive offsets of the depth-sorted Gaussians (offsets[e]) and, for every chunk of
+// kChunk output pairs, the first Gaussian whose pairs reach into it (chunk_first[c]);
+// chunk_first[n_chunks] = one past the last Gaussian with pairs.  Gaussians without pairs in
+// the strip carry the sentinel depth key, so they all sit after the last non-empty one.
+__global__ __launch_bounds__(kBlock) void k_scan_down(const uint32_t *__restrict__ perm,
+                                                      const uint32_t *__restrict__ strip_tiles,
+                                                      const uint32_t *__restrict__ partials,
+                                                      int64_t n, const uint64_t *__restrict__ total,
+                                                      uint32_t *__restrict__ offsets,
+                                                      uint32_t *__restrict__ chunk_first) {
     __shared__ uint32_t s_tmp[4];
     const int tid = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)tid * kItems;
-    uint32_t id[kItems], cnt[kItems], sum = 0;
+    uint32_t cnt[kItems], sum = 0;
 #pragma unroll
     for (int j = 0; j < kItems; ++j) {
         const int64_t e = base + j;
-        id[j] = e < n ? perm[e] : 0u;
-        cnt[j] = e < n ? strip_tiles[id[j]] : 0u;
+        cnt[j] = e < n ? strip_tiles[perm[e]] : 0u;
         sum += cnt[j];
     }
-    uint32_t total;
-    uint32_t off = block256_exclusive_scan(sum, s_tmp, total);
+    uint32_t blk_total;
+    uint32_t off = block256_exclusive_scan(sum, s_tmp, blk_total) + partials[blockIdx.x];
+    const uint32_t K = (uint32_t)*total;
+    const uint32_t n_chunks = (K + kChunk - 1) / kChunk;
 #pragma unroll
     for (int j = 0; j < kItems; ++j) {
-        const int le = tid * kItems + j;
-        uint32_t x0w = 0, row0 = 0;
+        const int64_t e = base + j;
+        if (e >= n) break;
+        offsets[e] = off;
         if (cnt[j]) {
-            const SplatRecord &r = records[id[j]];
-            const float4 ra = r.a;
-            const Rect rc = get_rect(ra.x, ra.y, __float_as_int(r.c.w), gx, gy);
-            x0w = rc.x0 | ((rc.x1 - rc.x0) << 16);
-            row0 = (max(rc.y0, row_begin) - row_begin) * gx;
+            for (uint32_t c = (off + kChunk - 1) / kChunk; c * kChunk < off + cnt[j]; ++c)
+                chunk_first[c] = (uint32_t)e;
+            if (off + cnt[j] == K) chunk_first[n_chunks] = (uint32_t)e + 1u;
         }
         off += cnt[j];
-        s_end[le] = off;
-        s_id[le] = id[j];
-        s_x0w[le] = x0w;
-        s_row0[le] = row0;
+    }
+}
+
+// Pass 4, upstream duplicateWithKeys, load-balanced by output: block c writes pairs
+// [c*kChunk, min(K, (c+1)*kChunk)) -- coalesced stores -- as (strip-local tile id, Gaussian
+// id), row-major over each Gaussian's rect like upstream.  The Gaussians overlapping the
+// chunk are staged in LDS; each output finds its owner by binary search over their offsets.
+__global__ __launch_bounds__(kBlock) void k_duplicate(
+    const uint32_t *__restrict__ perm, const uint32_t *__restrict__ offsets,
+    const uint32_t *__restrict__ chunk_first, uint32_t K, uint32_t n_chunks,
+    const SplatRecord *__restrict__ records, uint32_t gx, uint32_t gy, uint32_t row_begin,
+    uint32_t *__restrict__ tile_keys, uint32_t *__restrict__ tile_vals) {
+    __shared__ uint32_t s_off[kChunk + 1];
+    __shared__ uint32_t s_id[kChunk + 1];
+    __shared__ uint32_t s_x0w[kChunk + 1];   // rect x0 | width << 16
+    __shared__ uint32_t s_row0[kChunk + 1];  // first strip-local tile row * gx
+    const int tid = threadIdx.x;
+    const uint32_t c = blockIdx.x;
+    const uint32_t e_end_all = chunk_first[n_chunks];
+    const uint32_t e0 = chunk_first[c];
+    const uint32_t e1 = (c + 1 < n_chunks) ? min(chunk_first[c + 1] + 1u, e_end_all) : e_end_all;
+    const int ne = (int)(e1 - e0);  // <= kChunk + 1: every staged Gaussian owns >= 1 pair
+    for (int i = tid; i < ne; i += kBlock) {
+        const uint32_t id = perm[e0 + i];
+        const SplatRecord &r = records[id];
+        const float4 ra = r.a;
+        const Rect rc = get_rect(ra.x, ra.y, __float_as_int(r.c.w), gx, gy);
+        s_off[i] = offsets[e0 + i];
+        s_id[i] = id;
+        s_x0w[i] = rc.x0 | ((rc.x1 - rc.x0) << 16);
+        s_row0[i] = (max(rc.y0, row_begin) - row_begin) * gx;
     }
     __syncthreads();
-    const uint32_t gbase = partials[blockIdx.x];
-    for (uint32_t i = tid; i < total; i += kBlock) {
-        int lo = 0, hi = kTile - 1;  // first element whose inclusive end exceeds i
+    const uint32_t o_end = min(K, (c + 1) * kChunk);
+    for (uint32_t o = c * kChunk + tid; o < o_end; o += kBlock) {
+        int lo = 0, hi = ne - 1;  // last staged Gaussian whose offset <= o
         while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (s_end[mid] > i) hi = mid;
-            else lo = mid + 1;
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_off[mid] <= o) lo = mid;
+            else hi = mid - 1;
         }
-        const uint32_t first = lo > 0 ? s_end[lo - 1] : 0u;
-        const uint32_t local = i - first;
+        const uint32_t local = o - s_off[lo];
         const uint32_t x0w = s_x0w[lo];
         const uint32_t width = x0w >> 16;
         const uint32_t row = local / width;
         const uint32_t col = local - row * width;
-        tile_keys[gbase + i] = s_row0[lo] + row * gx + (x0w & 0xFFFFu) + col;
-        tile_vals[gbase + i] = s_id[lo];
+        tile_keys[o] = s_row0[lo] + row * gx + (x0w & 0xFFFFu) + col;
+        tile_vals[o] = s_id[lo];
     }
 }
 
@@ -161,14 +183,27 @@ hipError_t gsr_launch_scan_partials(uint32_t *partials, int64_t nb, uint64_t *to
     return hipGetLastError();
 }
 
-hipError_t gsr_launch_duplicate(const uint32_t *perm, const uint32_t *strip_tiles,
-                                const uint32_t *partials, int64_t n, const SplatRecord *records,
-                                uint32_t gx, uint32_t gy, uint32_t row_begin, uint32_t row_end,
-                                uint32_t *tile_keys, uint32_t *tile_vals, hipStream_t s) {
+hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint32_t *strip_tiles,
+                                const uint32_t *partials, int64_t n, const uint64_t *total,
+                                uint32_t *offsets, uint32_t *chunk_first, hipStream_t s) {
     const int64_t nb = gsr_scan_blocks(n);
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_duplicate, dim3((unsigned)nb), dim3(kBlock), 0, s, perm, strip_tiles,
-                       partials, n, records, gx, gy, row_begin, row_end, tile_keys, tile_vals);
+    hipLaunchKernelGGL(k_scan_down, dim3((unsigned)nb), dim3(kBlock), 0, s, perm, strip_tiles,
+                       partials, n, total, offsets, chunk_first);
+    return hipGetLastError();
+}
+
+int64_t gsr_duplicate_chunks(int64_t K) { return (K + kChunk - 1) / kChunk; }
+
+hipError_t gsr_launch_duplicate(const uint32_t *perm, const uint32_t *offsets,
+                                const uint32_t *chunk_first, int64_t K, const SplatRecord *records,
+                                uint32_t gx, uint32_t gy, uint32_t row_begin, uint32_t *tile_keys,
+                                uint32_t *tile_vals, hipStream_t s) {
+    const int64_t nc = gsr_duplicate_chunks(K);
+    if (nc == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_duplicate, dim3((unsigned)nc), dim3(kBlock), 0, s, perm, offsets,
+                       chunk_first, (uint32_t)K, (uint32_t)nc, records, gx, gy, row_begin,
+                       tile_keys, tile_vals);
     return hipGetLastError();
 }
 

@@ -237,11 +237,15 @@ hipError_t gsr_launch_scan_reduce(const uint32_t *perm, const uint32_t *strip_ti
                                   uint32_t *partials, hipStream_t s);
 hipError_t gsr_launch_scan_partials(uint32_t *partials, int64_t nb, uint64_t *total,
                                     hipStream_t s);
-hipError_t gsr_launch_duplicate(const uint32_t *perm, const uint32_t *strip_tiles,
-                                const uint32_t *partials, int64_t n,
+hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint32_t *strip_tiles,
+                                const uint32_t *partials, int64_t n, const uint64_t *total,
+                                uint32_t *offsets, uint32_t *chunk_first, hipStream_t s);
+int64_t gsr_duplicate_chunks(int64_t K);
+hipError_t gsr_launch_duplicate(const uint32_t *perm, const uint32_t *offsets,
+                                const uint32_t *chunk_first, int64_t K,
                                 const gsr::SplatRecord *records, uint32_t gx, uint32_t gy,
-                                uint32_t row_begin, uint32_t row_end, uint32_t *tile_keys,
-                                uint32_t *tile_vals, hipStream_t s);
+                                uint32_t row_begin, uint32_t *tile_keys, uint32_t *tile_vals,
+                                hipStream_t s);
 hipError_t gsr_launch_ranges(const uint32_t *tile_keys, int64_t K, uint32_t *ranges,
                              hipStream_t s);
 hipError_t gsr_launch_globalize_tiles(const uint32_t *local, int64_t K, uint32_t offset,
