@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--blend", default="fast", choices=["exact", "fast"],
+                    help="blend arithmetic: GSR_OPT_BLEND_FAST (default) or upstream's exact "
+                         "operation order")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="minimum CPU-oracle time to sample for cpu_baseline")
     return ap.parse_args()
@@ -146,13 +149,16 @@ def main():
             gather_strips(res.color, H, W, world, rank)
         return res
 
+    lib = _lib.load_library()
+    ctx = _lib.context(local)
+    _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_BLEND_FAST, int(args.blend == "fast")),
+               "gsr_set_option")
+
     # Warmup (also sizes the workspace so the timed loop never allocates).
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
 
-    lib = _lib.load_library()
-    ctx = _lib.context(local)
     _lib.check(lib.gsr_set_timing(ctx, 1), "gsr_set_timing")
     if world > 1:
         dist.barrier()
@@ -210,7 +216,8 @@ def main():
         "config": {"workload": f"{args.config}: {P} Gaussians, {W}x{H}, SH degree {scene.deg}, "
                                f"{scene.cam_kind} camera",
                    "gaussians": P, "width": W, "height": H, "sh_degree": scene.deg,
-                   "parallelism": f"image strips x{world}" + (" + RCCL gather" if world > 1 else "")},
+                   "parallelism": f"image strips x{world}" + (" + RCCL gather" if world > 1 else ""),
+                   "blend_arithmetic": args.blend},
         "msplats_per_sec": round(P * fps / 1e6, 2),
         "frame_stats": {"P_frustum": P_f, "P_visible": P_v, "K_pairs_mean": round(K_mean, 1),
                         "tiles": T_strip},

@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libgsr.so")
 ABI_VERSION = 1
 
 GSR_OPT_BLEND_CULL = 1
+GSR_OPT_BLEND_FAST = 2
 
 # Symbols include/gsr.h declares (checked by the CPU test suite).
 EXPORTED_SYMBOLS = (

@@ -55,6 +55,7 @@ struct gsr_context {
     uint32_t *last_point_list = nullptr, *last_tiles_local = nullptr;
     // options / timing
     int cull = 1;
+    int fast = 1;
     // Stage timing: a ring of event sets, one per forward, read back after the timed region.
     bool timing = false;
     int64_t timed_frames = 0;
@@ -188,6 +189,10 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
     if (!ctx) return fail(GSR_E_INVALID, "gsr_set_option: NULL context");
     if (option == GSR_OPT_BLEND_CULL) {
         ctx->cull = value ? 1 : 0;
+        return GSR_OK;
+    }
+    if (option == GSR_OPT_BLEND_FAST) {
+        ctx->fast = value ? 1 : 0;
         return GSR_OK;
     }
     return fail(GSR_E_INVALID, "gsr_set_option: unknown option " + std::to_string(option));
@@ -379,8 +384,8 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         GSR_HIP(gsr_launch_scan_down(perm, pa.strip_tiles, partials, P, d_total, offsets,
                                      chunk_first, s),
                 "scan_down launch");
-        GSR_HIP(gsr_launch_duplicate(perm, offsets, chunk_first, (int64_t)K, pa.records, gx, gy,
-                                     rb, tk, tv, s),
+        GSR_HIP(gsr_launch_duplicate(perm, offsets, chunk_first, (int64_t)K, pa.records,
+                                     out->radii, gx, gy, rb, tk, tv, s),
                 "duplicate launch");
     }
     GSR_TRY(stage_end(3));
@@ -415,6 +420,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     ba.final_T = out->final_T;
     ba.n_contrib = out->n_contrib;
     ba.cull = ctx->cull;
+    ba.fast = ctx->fast;
     GSR_HIP(gsr_launch_blend(ba, s), "blend launch");
     GSR_TRY(stage_end(6));
 

@@ -99,7 +99,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_down(const uint32_t *__restrict
 __global__ __launch_bounds__(kBlock) void k_duplicate(
     const uint32_t *__restrict__ perm, const uint32_t *__restrict__ offsets,
     const uint32_t *__restrict__ chunk_first, uint32_t K, uint32_t n_chunks,
-    const SplatRecord *__restrict__ records, uint32_t gx, uint32_t gy, uint32_t row_begin,
+    const SplatRecord *__restrict__ records, const int32_t *__restrict__ radii, uint32_t gx,
+    uint32_t gy, uint32_t row_begin,
     uint32_t *__restrict__ tile_keys, uint32_t *__restrict__ tile_vals) {
     __shared__ uint32_t s_off[kChunk + 1];
     __shared__ uint32_t s_id[kChunk + 1];
@@ -113,9 +114,8 @@ __global__ __launch_bounds__(kBlock) void k_duplicate(
     const int ne = (int)(e1 - e0);  // <= kChunk + 1: every staged Gaussian owns >= 1 pair
     for (int i = tid; i < ne; i += kBlock) {
         const uint32_t id = perm[e0 + i];
-        const SplatRecord &r = records[id];
-        const float4 ra = r.a;
-        const Rect rc = get_rect(ra.x, ra.y, __float_as_int(r.c.w), gx, gy);
+        const float4 ra = records[id].a;
+        const Rect rc = get_rect(ra.x, ra.y, radii[id], gx, gy);
         s_off[i] = offsets[e0 + i];
         s_id[i] = id;
         s_x0w[i] = rc.x0 | ((rc.x1 - rc.x0) << 16);
@@ -197,12 +197,13 @@ int64_t gsr_duplicate_chunks(int64_t K) { return (K + kChunk - 1) / kChunk; }
 
 hipError_t gsr_launch_duplicate(const uint32_t *perm, const uint32_t *offsets,
                                 const uint32_t *chunk_first, int64_t K, const SplatRecord *records,
-                                uint32_t gx, uint32_t gy, uint32_t row_begin, uint32_t *tile_keys,
+                                const int32_t *radii, uint32_t gx, uint32_t gy, uint32_t row_begin,
+                                uint32_t *tile_keys,
                                 uint32_t *tile_vals, hipStream_t s) {
     const int64_t nc = gsr_duplicate_chunks(K);
     if (nc == 0) return hipSuccess;
     hipLaunchKernelGGL(k_duplicate, dim3((unsigned)nc), dim3(kBlock), 0, s, perm, offsets,
-                       chunk_first, (uint32_t)K, (uint32_t)nc, records, gx, gy, row_begin,
+                       chunk_first, (uint32_t)K, (uint32_t)nc, records, radii, gx, gy, row_begin,
                        tile_keys, tile_vals);
     return hipGetLastError();
 }

@@ -8,13 +8,18 @@
 //
 // gfx950-specific structure:
 //  * cull once per staged splat, not once per (splat, wave): the loading thread tests the
-//    splat's conservative alpha >= 1/255 box against the tile's four quadrants and stores a
-//    4-bit mask; each wave then compacts the batch to the splats that can touch its quadrant
-//    (ballot + popcount) and loops over that list only;
+//    splat's conservative alpha >= 1/255 ellipse (preprocess.hip cull_data) against the tile's
+//    four 8x8 quadrants -- bounding box first, then the exact ellipse-box minimum with a
+//    rounding bound -- and stores a 4-bit mask; each wave then compacts the batch to the
+//    splats that can touch its quadrant (ballot + popcount) and loops over that list only;
 //  * branch-free per-pixel body (selects instead of nested ifs, so no exec-mask churn) with
 //    the LDS reads of the next splat issued before the current one is evaluated;
 //  * exp: the core of ocml's expf (range-reduced v_exp_f32 + ldexp), bit-identical to expf
-//    over the range that matters, without its under/overflow selects.
+//    over the range that matters, without its under/overflow selects;
+//  * optional fast arithmetic (GSR_OPT_BLEND_FAST): log2(e) and -1/2 folded into the conic at
+//    staging time, FMA-contracted quadratic form and the raw v_exp_f32 -- 2 of the 9 exp
+//    instructions and ~40 % of the per-pixel VALU work; pixels then differ from upstream's
+//    order by float rounding only.
 // The per-pixel arithmetic keeps upstream's operation order, so the image differs from the
 // CPU oracle only through expf itself (device vs glibc).  n_contrib equals upstream's running
 // `contributor` at the last contributing splat = its position in the tile list + 1, so
@@ -41,9 +46,35 @@ __device__ __forceinline__ float exp_core(float x) {
     return __builtin_ldexpf(e, (int)n);
 }
 
+// Lower bound of q(u, v) = A u^2 + 2B uv + C v^2 evaluated in float: q minus a bound on its
+// rounding error.
+__device__ __forceinline__ float q_lower(float A, float B, float C, float u, float v) {
+    const float uu = A * u * u, uv = 2.0f * B * u * v, vv = C * v * v;
+    return (uu + uv + vv) - 16.0f * 5.96e-8f * (uu + fabsf(uv) + vv);
+}
+
+// May the splat reach alpha >= 1/255 at some pixel centre of the box [bx0,bx1] x [by0,by1]?
+// False only when provably not (NaN / inf data always answer true).
+__device__ __forceinline__ bool may_touch(float x, float y, float A, float B, float C, float ex,
+                                          float ey, float twoL, float bx0, float bx1, float by0,
+                                          float by1) {
+    const float ulo = bx0 - x, uhi = bx1 - x, vlo = by0 - y, vhi = by1 - y;
+    if (fmaxf(fmaxf(ulo, -uhi), 0.0f) > ex || fmaxf(fmaxf(vlo, -vhi), 0.0f) > ey) return false;
+    if (ulo <= 0.0f && uhi >= 0.0f && vlo <= 0.0f && vhi >= 0.0f) return true;
+    // centre outside the box: q is convex, so its minimum over the box lies on an edge, where
+    // it is the 1-D minimum clamped to the edge
+    const float su = -B / C, sv = -B / A;
+    float lb = q_lower(A, B, C, ulo, fminf(fmaxf(su * ulo, vlo), vhi));
+    lb = fminf(lb, q_lower(A, B, C, uhi, fminf(fmaxf(su * uhi, vlo), vhi)));
+    lb = fminf(lb, q_lower(A, B, C, fminf(fmaxf(sv * vlo, ulo), uhi), vlo));
+    lb = fminf(lb, q_lower(A, B, C, fminf(fmaxf(sv * vhi, ulo), uhi), vhi));
+    return !(lb > twoL);
+}
+
+template <bool kFast>
 __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
-    __shared__ float4 s_geo[kBatch];   // x, y, conic.a, conic.b
-    __shared__ float4 s_opc[kBatch];   // conic.c, opacity, r, g
+    __shared__ float4 s_geo[kBatch];   // x, y, conic.a, conic.b   (fast: prescaled a, b)
+    __shared__ float4 s_opc[kBatch];   // conic.c, opacity, r, g    (fast: prescaled c)
     __shared__ float s_blue[kBatch];   // b
     __shared__ uint8_t s_mask[kBatch]; // quadrant bits of each staged splat
     __shared__ uint8_t s_list[4][kBatch];
@@ -65,24 +96,25 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
         const uint32_t idx = start + tid;
         if (idx < range.y) {
             const SplatRecord r = a.records[a.point_list[idx]];
-            s_geo[tid] = r.a;
-            s_opc[tid] = r.b;
-            s_blue[tid] = r.c.x;
             uint32_t m = 0xF;
             if (a.cull) {
-                // distance from the splat centre to each 8x8 quadrant, along x and y
-                const float x = r.a.x, y = r.a.y, ex = r.c.y, ey = r.c.z;
-                const float lx0 = (float)tx0, hx0 = (float)(tx0 + 7);
-                const float lx1 = (float)(tx0 + 8), hx1 = (float)(tx0 + 15);
-                const float ly0 = (float)ty0, hy0 = (float)(ty0 + 7);
-                const float ly1 = (float)(ty0 + 8), hy1 = (float)(ty0 + 15);
-                const bool inx0 = !(fmaxf(fmaxf(lx0 - x, x - hx0), 0.0f) > ex);
-                const bool inx1 = !(fmaxf(fmaxf(lx1 - x, x - hx1), 0.0f) > ex);
-                const bool iny0 = !(fmaxf(fmaxf(ly0 - y, y - hy0), 0.0f) > ey);
-                const bool iny1 = !(fmaxf(fmaxf(ly1 - y, y - hy1), 0.0f) > ey);
-                m = (uint32_t)(inx0 && iny0) | ((uint32_t)(inx1 && iny0) << 1) |
-                    ((uint32_t)(inx0 && iny1) << 2) | ((uint32_t)(inx1 && iny1) << 3);
+                const float x = r.a.x, y = r.a.y, A = r.a.z, B = r.a.w, C = r.b.x;
+                const float ex = r.c.y, ey = r.c.z, twoL = 2.0f * r.c.w;
+                const float X0 = (float)tx0, Y0 = (float)ty0;
+                m = (uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0, X0 + 7, Y0, Y0 + 7) |
+                    ((uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0 + 8, X0 + 15, Y0, Y0 + 7) << 1) |
+                    ((uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0, X0 + 7, Y0 + 8, Y0 + 15) << 2) |
+                    ((uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0 + 8, X0 + 15, Y0 + 8, Y0 + 15) << 3);
             }
+            if (kFast) {
+                const float kL2e = 1.4426950408889634f;
+                s_geo[tid] = make_float4(r.a.x, r.a.y, r.a.z * (-0.5f * kL2e), r.a.w * (-kL2e));
+                s_opc[tid] = make_float4(r.b.x * (-0.5f * kL2e), r.b.y, r.b.z, r.b.w);
+            } else {
+                s_geo[tid] = r.a;
+                s_opc[tid] = r.b;
+            }
+            s_blue[tid] = r.c.x;
             s_mask[tid] = (uint8_t)m;
         }
         __syncthreads();
@@ -109,17 +141,33 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
             const int jn = s_list[w][k + 1 < count ? k + 1 : k];
             const float4 g_next = s_geo[jn], q_next = s_opc[jn];
             const float blue_next = s_blue[jn];
-            // upstream renderCUDA per-pixel body, same operation order
             const float dx = g.x - pfx, dy = g.y - pfy;
-            const float power = -0.5f * (g.z * dx * dx + q.x * dy * dy) - g.w * dx * dy;
-            const float alpha = fminf(0.99f, q.y * exp_core(power));
+            bool live;
+            float alpha;
+            if (kFast) {
+                // log2(e) * power with the constants folded in: dx (a dx + b dy) + c dy^2
+                const float p2 = __builtin_fmaf(dx, __builtin_fmaf(g.z, dx, g.w * dy), q.x * dy * dy);
+                alpha = fminf(0.99f, q.y * __builtin_amdgcn_exp2f(p2));
+                live = !done && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+            } else {
+                // upstream renderCUDA per-pixel body, same operation order
+                const float power = -0.5f * (g.z * dx * dx + q.x * dy * dy) - g.w * dx * dy;
+                alpha = fminf(0.99f, q.y * exp_core(power));
+                live = !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+            }
             const float test_T = T * (1 - alpha);
-            const bool live = !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
             const bool term = live && (test_T < 0.0001f);
             const bool acc = live && !(test_T < 0.0001f);
-            C0 = acc ? C0 + q.z * alpha * T : C0;
-            C1 = acc ? C1 + q.w * alpha * T : C1;
-            C2 = acc ? C2 + blue * alpha * T : C2;
+            if (kFast) {
+                const float wgt = acc ? alpha * T : 0.0f;
+                C0 = __builtin_fmaf(q.z, wgt, C0);
+                C1 = __builtin_fmaf(q.w, wgt, C1);
+                C2 = __builtin_fmaf(blue, wgt, C2);
+            } else {
+                C0 = acc ? C0 + q.z * alpha * T : C0;
+                C1 = acc ? C1 + q.w * alpha * T : C1;
+                C2 = acc ? C2 + blue * alpha * T : C2;
+            }
             T = acc ? test_T : T;
             last_contributor = acc ? start - range.x + (uint32_t)j + 1u : last_contributor;
             done = done || term;
@@ -147,6 +195,9 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
 
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s) {
     if (a.rows_tiles == 0 || a.grid_x == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_blend, dim3(a.grid_x, a.rows_tiles), dim3(256), 0, s, a);
+    if (a.fast)
+        hipLaunchKernelGGL(k_blend<true>, dim3(a.grid_x, a.rows_tiles), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_blend<false>, dim3(a.grid_x, a.rows_tiles), dim3(256), 0, s, a);
     return hipGetLastError();
 }

@@ -19,7 +19,8 @@ namespace gsr {
 
 // One visible Gaussian as the blend consumes it: 48 B, three 16-B loads, written by the
 // preprocess, gathered by tile lists.  a = {x, y, conic.a, conic.b}; b = {conic.c, opacity,
-// r, g}; c = {b, cull_ex, cull_ey, radius (int bits)}.
+// r, g}; c = {b, cull_ex, cull_ey, cull_Lm} (conservative alpha >= 1/255 region, see
+// preprocess.hip cull_data).
 struct alignas(16) SplatRecord {
     float4 a, b, c;
 };
@@ -243,7 +244,8 @@ hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint32_t *strip_tile
 int64_t gsr_duplicate_chunks(int64_t K);
 hipError_t gsr_launch_duplicate(const uint32_t *perm, const uint32_t *offsets,
                                 const uint32_t *chunk_first, int64_t K,
-                                const gsr::SplatRecord *records, uint32_t gx, uint32_t gy,
+                                const gsr::SplatRecord *records, const int32_t *radii,
+                                uint32_t gx, uint32_t gy,
                                 uint32_t row_begin, uint32_t *tile_keys, uint32_t *tile_vals,
                                 hipStream_t s);
 hipError_t gsr_launch_ranges(const uint32_t *tile_keys, int64_t K, uint32_t *ranges,
@@ -262,5 +264,6 @@ struct GsrBlendArgs {
     float *out_color, *final_T;
     uint32_t *n_contrib;
     int cull;
+    int fast;  // 1: folded-constant FMA arithmetic + raw v_exp_f32 (see blend.hip)
 };
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s);

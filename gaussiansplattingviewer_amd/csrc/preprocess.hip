@@ -6,7 +6,8 @@
 // xyz (12 B) for every point, scale/rot/opacity (32 B) for points in front of the camera
 // and SH (192 B at degree 3) only for points that survive culling; it writes one 48-B
 // SplatRecord for visible points plus the 8-B (key, id) pair of the depth sort and 8 B of
-// radius / strip tile count.
+// radius / strip tile count.  SplatRecord: a = {x, y, conic.a, conic.b}, b = {conic.c,
+// opacity, r, g}, c = {b, cull ex, cull ey, cull Lm}.
 #include "gsr_internal.h"
 
 using namespace gsr;
@@ -93,15 +94,18 @@ __device__ __forceinline__ float3 color_from_sh(float3 pos, const float *campos,
     return make_float3(fmaxf(r0, 0.0f), fmaxf(r1, 0.0f), fmaxf(r2, 0.0f));
 }
 
-// Conservative half-extents (pixels) of the region where this splat can reach
-// alpha >= 1/255: o*exp(power) >= 1/255  <=>  q(d) = A dx^2 + 2B dx dy + C dy^2 <= 2 ln(255 o).
-// The box is computed in double from the float conic the blend evaluates, widened by an
-// absolute bound on the float rounding of `power` and by a pixel margin.  It is only used
-// by the blend to skip whole waves; outputs are identical with and without it (tested).
-__device__ __forceinline__ float2 cull_extent(float A, float B, float C, float o) {
+// Conservative cull data of one splat for the blend: the region where it can reach
+// alpha >= 1/255 is  q(d) = A dx^2 + 2B dx dy + C dy^2 <= 2 L,  L = ln(255 o)  (upstream
+// alpha = min(0.99, o exp(power)), power = -q/2).  Returns {ex, ey, Lm}: Lm >= L widened by an
+// absolute bound on the float rounding of the blend's `power` inside the box plus margins, and
+// the half-extents (pixels) of the ellipse q <= 2 Lm.  Computed in double from the float conic
+// the blend evaluates.  Used only to skip (splat, 8x8 quadrant) pairs that provably cannot
+// contribute; outputs are identical with and without it (tested).
+__device__ __forceinline__ float3 cull_data(float A, float B, float C, float o) {
     const float kInf = __builtin_huge_valf();
     const double det = (double)A * (double)C - (double)B * (double)B;
-    if (!(det > 0.0) || !(A > 0.0f) || !(C > 0.0f) || !(o == o)) return make_float2(kInf, kInf);
+    if (!(det > 0.0) || !(A > 0.0f) || !(C > 0.0f) || !(o == o))
+        return make_float3(kInf, kInf, kInf);
     double L = log(255.0 * (double)o);
     if (L < 0.0) L = 0.0;
     const double sxx = (double)C / det, syy = (double)A / det;  // inverse of the conic
@@ -111,8 +115,9 @@ __device__ __forceinline__ float2 cull_extent(float A, float B, float C, float o
     const double Lm = (L + 8.0 * 5.96e-8 * mag + 1e-3) * 1.01;
     ex = sqrt(2.0 * Lm * sxx) + 0.02;
     ey = sqrt(2.0 * Lm * syy) + 0.02;
-    if (!(ex < 1e30) || !(ey < 1e30)) return make_float2(kInf, kInf);
-    return make_float2((float)ex, (float)ey);
+    if (!(ex < 1e30) || !(ey < 1e30) || !(Lm < 1e30)) return make_float3(kInf, kInf, kInf);
+    // round Lm up: one ulp above its float conversion (Lm > 0 and finite here)
+    return make_float3((float)ex, (float)ey, __uint_as_float(__float_as_uint((float)Lm) + 1u));
 }
 
 __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
@@ -170,11 +175,11 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
                 const uint32_t sy0 = max(rc.y0, a.row_begin), sy1 = min(rc.y1, a.row_end);
                 strip_tiles = sy1 > sy0 ? (rc.x1 - rc.x0) * (sy1 - sy0) : 0u;
                 if (strip_tiles) key = __float_as_uint(p_view.z);  // z > 0.2: bits are monotone
-                const float2 ext = cull_extent(conic_a, conic_b, conic_c, opacity);
+                const float3 cd = cull_data(conic_a, conic_b, conic_c, opacity);
                 SplatRecord rec;
                 rec.a = make_float4(px, py, conic_a, conic_b);
                 rec.b = make_float4(conic_c, opacity, col.x, col.y);
-                rec.c = make_float4(col.z, ext.x, ext.y, __int_as_float(r_int));
+                rec.c = make_float4(col.z, cd.x, cd.y, cd.z);
                 a.records[idx] = rec;
                 if (a.depths) a.depths[idx] = p_view.z;
                 if (a.means2D) {

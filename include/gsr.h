@@ -135,9 +135,14 @@ int gsr_set_timing(gsr_context *ctx, int enable);
 int gsr_stage_times(gsr_context *ctx, float *ms, int n);
 const char *gsr_stage_name(int i);
 
-/* Tuning / verification switches.  GSR_OPT_BLEND_CULL (default 1): per-wave conservative
- * ellipse cull in the blend; outputs are bit-identical either way (tested). */
-enum { GSR_OPT_BLEND_CULL = 1 };
+/* Tuning / verification switches.
+ *   GSR_OPT_BLEND_CULL (default 1): conservative ellipse-vs-quadrant cull in the blend;
+ *     outputs are bit-identical either way (tested).
+ *   GSR_OPT_BLEND_FAST (default 1): blend arithmetic with log2(e) folded into the conic, FMA
+ *     contraction and the hardware exp2; changes pixels by float rounding only (tolerance in
+ *     tests/gpu_helpers.py).  0 keeps upstream's per-pixel operation order (IEEE, no FMA,
+ *     ocml expf). */
+enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
 
 #ifdef __cplusplus
