@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sort-shape", type=int, default=None, help="GSR_OPT_TILE_SORT_SHAPE (tuning)")
+    ap.add_argument("--onesweep", action="store_true", help="GSR_OPT_SORT_ONESWEEP (tuning)")
     ap.add_argument("--blend", default="fast", choices=["exact", "fast"],
                     help="blend arithmetic: GSR_OPT_BLEND_FAST (default) or upstream's exact "
                          "operation order")
@@ -153,6 +155,10 @@ def main():
     ctx = _lib.context(local)
     _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_BLEND_FAST, int(args.blend == "fast")),
                "gsr_set_option")
+    if args.sort_shape is not None:
+        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_TILE_SORT_SHAPE, args.sort_shape), "opt")
+    if args.onesweep:
+        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_SORT_ONESWEEP, 1), "opt")
 
     # Warmup (also sizes the workspace so the timed loop never allocates).
     for i in range(args.warmup):

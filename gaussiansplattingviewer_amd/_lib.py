@@ -15,6 +15,8 @@ ABI_VERSION = 1
 
 GSR_OPT_BLEND_CULL = 1
 GSR_OPT_BLEND_FAST = 2
+GSR_OPT_SORT_ONESWEEP = 3
+GSR_OPT_TILE_SORT_SHAPE = 4
 
 # Symbols include/gsr.h declares (checked by the CPU test suite).
 EXPORTED_SYMBOLS = (

@@ -44,6 +44,10 @@ struct gsr_context {
     // per-Gaussian workspace
     DevBuf records, strip_tiles, sort_keys, sort_vals, sort_keys_alt, sort_vals_alt, partials,
         total, hist, digit_total, offsets, chunk_first;
+    // onesweep sort state: [0,1024) depth-sort digit counts, [1024,2048) tile-sort counts,
+    // then the ticket word; look-back granules
+    DevBuf sort_ctl, status;
+    uint32_t epoch = 0;  // tags the look-back granules of every onesweep pass
     // per-pair workspace
     DevBuf tile_keys, tile_vals, tile_keys_alt, tile_vals_alt;
     DevBuf ranges_local;
@@ -56,6 +60,8 @@ struct gsr_context {
     // options / timing
     int cull = 1;
     int fast = 1;
+    int onesweep = 0;
+    int tile_sort_shape = 3;  // 8 waves x 8 keys/lane: fastest measured
     // Stage timing: a ring of event sets, one per forward, read back after the timed region.
     bool timing = false;
     int64_t timed_frames = 0;
@@ -86,6 +92,15 @@ int grow(gsr_context *ctx, DevBuf &b, size_t bytes, hipStream_t s) {
     return GSR_OK;
 }
 
+// Grow-only buffer whose contents must start at zero (look-back granules, ticket).
+int grow_zeroed(gsr_context *ctx, DevBuf &b, size_t bytes, hipStream_t s) {
+    const void *before = b.p;
+    int rc = grow(ctx, b, bytes, s);
+    if (rc != GSR_OK) return rc;
+    if (b.p != before) GSR_HIP(hipMemsetAsync(b.p, 0, b.cap, s), "hipMemsetAsync(zero-init)");
+    return GSR_OK;
+}
+
 #define GSR_TRY(expr)                 \
     do {                              \
         int rc_ = (expr);             \
@@ -101,10 +116,12 @@ int reserve_P(gsr_context *ctx, int64_t P, hipStream_t s) {
     GSR_TRY(grow(ctx, ctx->sort_keys_alt, n * 4, s));
     GSR_TRY(grow(ctx, ctx->sort_vals_alt, n * 4, s));
     GSR_TRY(grow(ctx, ctx->partials, (size_t)std::max<int64_t>(gsr_scan_blocks(P), 1) * 4, s));
-    GSR_TRY(grow(ctx, ctx->total, 16, s));
+    GSR_TRY(grow_zeroed(ctx, ctx->total, 16, s));  // [K (u64), look-back error flag (u32)]
     GSR_TRY(grow(ctx, ctx->hist, (size_t)gsr_radix_hist_words(P) * 4, s));
     GSR_TRY(grow(ctx, ctx->digit_total, 256 * 4, s));
     GSR_TRY(grow(ctx, ctx->offsets, n * 4, s));
+    GSR_TRY(grow_zeroed(ctx, ctx->sort_ctl, 2048 * 4 + 256, s));
+    GSR_TRY(grow_zeroed(ctx, ctx->status, (size_t)gsr_onesweep_status_words(P) * 8, s));
     return GSR_OK;
 }
 
@@ -116,6 +133,26 @@ int reserve_K(gsr_context *ctx, int64_t K, hipStream_t s) {
     GSR_TRY(grow(ctx, ctx->tile_vals_alt, n * 4, s));
     GSR_TRY(grow(ctx, ctx->hist, (size_t)gsr_radix_hist_words(K) * 4, s));
     GSR_TRY(grow(ctx, ctx->chunk_first, (size_t)(gsr_duplicate_chunks(K) + 1) * 4, s));
+    GSR_TRY(grow_zeroed(ctx, ctx->status, (size_t)gsr_onesweep_status_words(K) * 8, s));
+    return GSR_OK;
+}
+
+GsrOnesweepWs onesweep_ws(gsr_context *ctx, int which) {
+    uint32_t *ctl = static_cast<uint32_t *>(ctx->sort_ctl.p);
+    GsrOnesweepWs ws;
+    ws.ghist = ctl + 1024 * which;
+    ws.ticket = ctl + 2048;
+    ws.err = static_cast<uint32_t *>(ctx->total.p) + 2;  // after the 64-bit K
+    ws.status = static_cast<uint64_t *>(ctx->status.p);
+    ws.epoch = &ctx->epoch;
+    return ws;
+}
+
+// Keeps the 31-bit granule epoch from wrapping into old tags: re-zero the granules first.
+int epoch_guard(gsr_context *ctx, int passes, hipStream_t s) {
+    if (ctx->epoch + (uint32_t)passes < 0x7FFFFFF0u) return GSR_OK;
+    GSR_HIP(hipMemsetAsync(ctx->status.p, 0, ctx->status.cap, s), "hipMemsetAsync(granules)");
+    ctx->epoch = 0;
     return GSR_OK;
 }
 
@@ -142,7 +179,7 @@ int gsr_create(gsr_context **out) {
         delete ctx;
         return fail(GSR_E_HIP, "gsr_create: no HIP device");
     }
-    if (hipHostMalloc(reinterpret_cast<void **>(&ctx->h_total), sizeof(uint64_t)) != hipSuccess) {
+    if (hipHostMalloc(reinterpret_cast<void **>(&ctx->h_total), 2 * sizeof(uint64_t)) != hipSuccess) {
         (void)hipGetLastError();
         delete ctx;
         return fail(GSR_E_HIP, "gsr_create: hipHostMalloc failed");
@@ -166,6 +203,7 @@ void gsr_destroy(gsr_context *ctx) {
                       &ctx->sort_vals,     &ctx->sort_keys_alt, &ctx->sort_vals_alt,
                       &ctx->partials,      &ctx->total,         &ctx->hist,
                       &ctx->digit_total,   &ctx->offsets,       &ctx->chunk_first,
+                      &ctx->sort_ctl,      &ctx->status,
                       &ctx->tile_keys,     &ctx->tile_vals,
                       &ctx->tile_keys_alt, &ctx->tile_vals_alt, &ctx->ranges_local};
     for (DevBuf *b : bufs)
@@ -193,6 +231,15 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
     }
     if (option == GSR_OPT_BLEND_FAST) {
         ctx->fast = value ? 1 : 0;
+        return GSR_OK;
+    }
+    if (option == GSR_OPT_SORT_ONESWEEP) {
+        ctx->onesweep = value ? 1 : 0;
+        return GSR_OK;
+    }
+    if (option == GSR_OPT_TILE_SORT_SHAPE) {
+        if (value < 0 || value > 4) return fail(GSR_E_INVALID, "gsr_set_option: shape 0..4");
+        ctx->tile_sort_shape = (int)value;
         return GSR_OK;
     }
     return fail(GSR_E_INVALID, "gsr_set_option: unknown option " + std::to_string(option));
@@ -353,8 +400,17 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     uint32_t *dv_alt = static_cast<uint32_t *>(ctx->sort_vals_alt.p);
     uint32_t *hist = static_cast<uint32_t *>(ctx->hist.p);
     uint32_t *digit_total = static_cast<uint32_t *>(ctx->digit_total.p);
-    GSR_HIP(gsr_radix_sort_pairs(&dk, &dv, &dk_alt, &dv_alt, P, 0, 32, hist, digit_total, s),
-            "depth sort launch");
+    if (ctx->onesweep) {
+        GSR_TRY(epoch_guard(ctx, 8, s));
+        // zero both digit-count blocks (depth + tile sort) once per frame
+        GSR_HIP(hipMemsetAsync(ctx->sort_ctl.p, 0, 2048 * 4, s), "hipMemsetAsync(digit counts)");
+        GSR_HIP(gsr_onesweep_sort(&dk, &dv, &dk_alt, &dv_alt, P, 0, 32, GSR_HIST_COUNT,
+                                  onesweep_ws(ctx, 0), s),
+                "depth sort launch");
+    } else {
+        GSR_HIP(gsr_radix_sort_pairs(&dk, &dv, &dk_alt, &dv_alt, P, 0, 32, hist, digit_total, s),
+                "depth sort launch");
+    }
     GSR_TRY(stage_end(1));
     const uint32_t *perm = dv;
 
@@ -363,16 +419,19 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     uint64_t *d_total = static_cast<uint64_t *>(ctx->total.p);
     GSR_HIP(gsr_launch_scan_reduce(perm, pa.strip_tiles, P, partials, s), "scan launch");
     GSR_HIP(gsr_launch_scan_partials(partials, gsr_scan_blocks(P), d_total, s), "scan launch");
-    GSR_HIP(hipMemcpyAsync(ctx->h_total, d_total, sizeof(uint64_t), hipMemcpyDeviceToHost, s),
+    GSR_HIP(hipMemcpyAsync(ctx->h_total, d_total, 16, hipMemcpyDeviceToHost, s),
             "hipMemcpyAsync(num_rendered)");
     GSR_TRY(stage_end(2));
     GSR_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(num_rendered)");
-    const uint64_t K = *ctx->h_total;
+    const uint64_t K = ctx->h_total[0];
+    if (ctx->h_total[1] != 0)
+        return fail(GSR_E_HIP, "gsr_forward: radix sort look-back gave up (device flag set)");
     if (K > (uint64_t)UINT32_MAX - 4096)
         return fail(GSR_E_INVALID, "gsr_forward: more than 2^32-4097 (Gaussian, tile) pairs");
     GSR_TRY(reserve_K(ctx, (int64_t)K, s));
 
     // ---- 4. duplicate into (tile, Gaussian) pairs, depth order, load-balanced by output ------
+    const int tbits = T_strip > 1 ? bits_for(T_strip - 1) : 0;
     uint32_t *tk = static_cast<uint32_t *>(ctx->tile_keys.p);
     uint32_t *tv = static_cast<uint32_t *>(ctx->tile_vals.p);
     uint32_t *tk_alt = static_cast<uint32_t *>(ctx->tile_keys_alt.p);
@@ -384,17 +443,25 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         GSR_HIP(gsr_launch_scan_down(perm, pa.strip_tiles, partials, P, d_total, offsets,
                                      chunk_first, s),
                 "scan_down launch");
+        // the onesweep tile sort takes its digit counts from the duplicate (fused)
         GSR_HIP(gsr_launch_duplicate(perm, offsets, chunk_first, (int64_t)K, pa.records,
-                                     out->radii, gx, gy, rb, tk, tv, s),
+                                     out->radii, gx, gy, rb, tk, tv,
+                                     ctx->onesweep ? gsr_radix_plan(0, tbits) : GsrRadixPlan{},
+                                     onesweep_ws(ctx, 1).ghist, s),
                 "duplicate launch");
     }
     GSR_TRY(stage_end(3));
 
     // ---- 5. stable radix sort of the pairs by (strip-local) tile id -------------------------
-    const int tbits = T_strip > 1 ? bits_for(T_strip - 1) : 0;
-    GSR_HIP(gsr_radix_sort_pairs(&tk, &tv, &tk_alt, &tv_alt, (int64_t)K, 0, tbits, hist,
-                                 digit_total, s),
-            "tile sort launch");
+    if (ctx->onesweep) {
+        GSR_HIP(gsr_onesweep_sort(&tk, &tv, &tk_alt, &tv_alt, (int64_t)K, 0, tbits,
+                                  K > 0 ? GSR_HIST_READY : GSR_HIST_COUNT, onesweep_ws(ctx, 1), s),
+                "tile sort launch");
+    } else {
+        GSR_HIP(gsr_radix_sort_pairs(&tk, &tv, &tk_alt, &tv_alt, (int64_t)K, 0, tbits, hist,
+                                     digit_total, s, ctx->tile_sort_shape),
+                "tile sort launch");
+    }
     GSR_TRY(stage_end(4));
 
     // ---- 6. tile ranges ----------------------------------------------------------------------
@@ -489,9 +556,17 @@ int gsr_depth_argsort(gsr_context *ctx, const float *xyz, int64_t P, const float
     GSR_HIP(gsr_launch_view_depth_keys(xyz, P, view_host16[8], view_host16[9], view_host16[10],
                                        view_host16[11], k, v, out_depth, s),
             "view depth launch");
-    GSR_HIP(gsr_radix_sort_pairs(&k, &v, &ka, &va, P, 0, 32, static_cast<uint32_t *>(ctx->hist.p),
-                                 static_cast<uint32_t *>(ctx->digit_total.p), s),
-            "depth argsort launch");
+    if (ctx->onesweep) {
+        GSR_TRY(epoch_guard(ctx, 4, s));
+        GSR_HIP(gsr_onesweep_sort(&k, &v, &ka, &va, P, 0, 32, GSR_HIST_ZERO_AND_COUNT,
+                                  onesweep_ws(ctx, 0), s),
+                "depth argsort launch");
+    } else {
+        GSR_HIP(gsr_radix_sort_pairs(&k, &v, &ka, &va, P, 0, 32,
+                                     static_cast<uint32_t *>(ctx->hist.p),
+                                     static_cast<uint32_t *>(ctx->digit_total.p), s),
+                "depth argsort launch");
+    }
     GSR_HIP(gsr_launch_index_to_i32(v, P, out_index, s), "index launch");
     return GSR_OK;
 }

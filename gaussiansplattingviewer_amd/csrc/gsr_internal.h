@@ -227,9 +227,36 @@ hipError_t gsr_launch_index_to_i32(const uint32_t *vals, int64_t P, int32_t *out
 // On return *keys / *vals point at the buffers holding the sorted data (either the input
 // pair or the alt pair).  hist needs gsr_radix_hist_words(n) words.
 int64_t gsr_radix_hist_words(int64_t n);
+// shape: tile shape (waves x items per lane): 0 = 4x16, 1 = 16x16, 2 = 4x8, 3 = 8x8, 4 = 8x16.
 hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
                                 uint32_t **vals_alt, int64_t n, int begin_bit, int end_bit,
-                                uint32_t *hist, uint32_t *digit_total, hipStream_t s);
+                                uint32_t *hist, uint32_t *digit_total, hipStream_t s,
+                                int shape = 0);
+
+// Onesweep radix sort (one kernel per pass, decoupled look-back).  Pass plan: the key bits
+// [begin, end) split into n <= 4 passes of <= 8 bits.  ghist holds the global digit counts of
+// every pass ([pass][256]); hist_ready = the caller already accumulated them (fused into the
+// kernel that produced the keys, e.g. k_duplicate) -- see hist_state.
+#define GSR_RADIX_MAX_PASSES 4
+struct GsrRadixPlan {
+    int n;
+    int shift[GSR_RADIX_MAX_PASSES];
+    int nbits[GSR_RADIX_MAX_PASSES];
+    uint32_t mask[GSR_RADIX_MAX_PASSES];
+};
+struct GsrOnesweepWs {
+    uint32_t *ghist;   // [GSR_RADIX_MAX_PASSES][256]
+    uint64_t *status;  // gsr_onesweep_status_words(n) granules, zero-initialised once
+    uint32_t *ticket;  // one word, zero-initialised once (rewound by every pass)
+    uint32_t *err;     // look-back give-up flag
+    uint32_t *epoch;   // HOST counter, tags every pass's granules
+};
+GsrRadixPlan gsr_radix_plan(int begin_bit, int end_bit);
+int64_t gsr_onesweep_status_words(int64_t n);
+enum { GSR_HIST_ZERO_AND_COUNT = 0, GSR_HIST_COUNT = 1, GSR_HIST_READY = 2 };
+hipError_t gsr_onesweep_sort(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
+                             uint32_t **vals_alt, int64_t n, int begin_bit, int end_bit,
+                             int hist_state, const GsrOnesweepWs &ws, hipStream_t s);
 
 // Binning: offsets scan over depth-sorted strip tile counts, duplicate into (tile, id)
 // pairs, and tile ranges.
@@ -247,7 +274,7 @@ hipError_t gsr_launch_duplicate(const uint32_t *perm, const uint32_t *offsets,
                                 const gsr::SplatRecord *records, const int32_t *radii,
                                 uint32_t gx, uint32_t gy,
                                 uint32_t row_begin, uint32_t *tile_keys, uint32_t *tile_vals,
-                                hipStream_t s);
+                                const GsrRadixPlan &plan, uint32_t *ghist, hipStream_t s);
 hipError_t gsr_launch_ranges(const uint32_t *tile_keys, int64_t K, uint32_t *ranges,
                              hipStream_t s);
 hipError_t gsr_launch_globalize_tiles(const uint32_t *local, int64_t K, uint32_t offset,

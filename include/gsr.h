@@ -142,7 +142,13 @@ const char *gsr_stage_name(int i);
  *     contraction and the hardware exp2; changes pixels by float rounding only (tolerance in
  *     tests/gpu_helpers.py).  0 keeps upstream's per-pixel operation order (IEEE, no FMA,
  *     ocml expf). */
-enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2 };
+/*   GSR_OPT_SORT_ONESWEEP (default 0): 1 = one-kernel-per-pass radix sort with decoupled
+ *     look-back; 0 = reduce-then-scan (identical results; faster on MI355X at these sizes,
+ *     see DESIGN.md). */
+/*   GSR_OPT_TILE_SORT_SHAPE (tuning): tile shape of the pair sort's reduce-then-scan kernels,
+ *     0 = 4 waves x 16 keys/lane, 1 = 16x16, 2 = 4x8, 3 = 8x8 (default), 4 = 8x16. */
+enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_SORT_ONESWEEP = 3,
+       GSR_OPT_TILE_SORT_SHAPE = 4 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
 
 #ifdef __cplusplus

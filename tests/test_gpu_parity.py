@@ -211,3 +211,16 @@ def test_headline_config_c3(gpu, c3_oracle, fast):
         _set_option(gpu, _lib.GSR_OPT_BLEND_FAST, 1)
     assert orc["num_rendered"] > 5_000_000
     assert_parity(hip, orc)
+
+
+def test_sort_implementations_agree(gpu):
+    """Reduce-then-scan (default) and onesweep radix sorts give identical binning."""
+    s = scene_inputs(synthetic_gaussians(300_000, 3, 21), static_camera(1920, 1080, (0.5, 0.2, 3.5)), 3)
+    rts = run_hip(s, gpu)
+    _set_option(gpu, _lib.GSR_OPT_SORT_ONESWEEP, 1)
+    try:
+        one = run_hip(s, gpu)
+    finally:
+        _set_option(gpu, _lib.GSR_OPT_SORT_ONESWEEP, 0)
+    for k in ("point_list", "point_tiles", "ranges", "color", "n_contrib"):
+        np.testing.assert_array_equal(one[k], rts[k], err_msg=k)

@@ -17,17 +17,23 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    m = re.search(r"::(k_[a-z0-9_]+)", name)
+    m = re.search(r"::(k_[a-z0-9_]+)(<[^>]*>)?", name)
     if m:
-        return m.group(1)
+        return m.group(1) + (m.group(2) or "")
     return name.split("(")[0][:60]
 
 
 def load_stats(d):
     path = os.path.join(d, "trace", "trace_kernel_stats.csv")
-    rows = list(csv.DictReader(open(path)))
-    return {short(r["Name"]): (int(r["Calls"]), float(r["AverageNs"]), float(r["TotalDurationNs"]))
-            for r in rows}
+    out = {}
+    for r in csv.DictReader(open(path)):
+        k = short(r["Name"])
+        c, t = int(r["Calls"]), float(r["TotalDurationNs"])
+        if k in out:
+            c0, _, t0 = out[k]
+            c, t = c + c0, t + t0
+        out[k] = (c, t / c, t)
+    return out
 
 
 def load_trace(d):
