@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sort-shape", type=int, default=None, help="GSR_OPT_TILE_SORT_SHAPE (tuning)")
     ap.add_argument("--onesweep", action="store_true", help="GSR_OPT_SORT_ONESWEEP (tuning)")
-    ap.add_argument("--blend", default="fast", choices=["exact", "fast"],
+    ap.add_argument("--blend", default="fast", choices=["exact", "fast", "packed"],
                     help="blend arithmetic: GSR_OPT_BLEND_FAST (default) or upstream's exact "
                          "operation order")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -153,7 +153,8 @@ def main():
 
     lib = _lib.load_library()
     ctx = _lib.context(local)
-    _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_BLEND_FAST, int(args.blend == "fast")),
+    _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_BLEND_FAST,
+                                  {"exact": 0, "fast": 1, "packed": 2}[args.blend]),
                "gsr_set_option")
     if args.sort_shape is not None:
         _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_TILE_SORT_SHAPE, args.sort_shape), "opt")

@@ -230,7 +230,8 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
         return GSR_OK;
     }
     if (option == GSR_OPT_BLEND_FAST) {
-        ctx->fast = value ? 1 : 0;
+        if (value < 0 || value > 2) return fail(GSR_E_INVALID, "gsr_set_option: fast 0..2");
+        ctx->fast = (int)value;
         return GSR_OK;
     }
     if (option == GSR_OPT_SORT_ONESWEEP) {

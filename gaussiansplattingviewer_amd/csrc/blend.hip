@@ -30,7 +30,6 @@ using namespace gsr;
 
 namespace {
 
-constexpr int kBatch = 256;
 
 // ocml __ocml_exp_f32 (non-DAZ path) without the final range selects: identical results for
 // every finite argument (below about -104 both give 0, above 88.7 both give +inf).
@@ -70,6 +69,10 @@ __device__ __forceinline__ bool may_touch(float x, float y, float A, float B, fl
     lb = fminf(lb, q_lower(A, B, C, fminf(fmaxf(sv * vhi, ulo), uhi), vhi));
     return !(lb > twoL);
 }
+
+constexpr int kBatch = 256;  // splats staged in LDS per round
+
+typedef float v2f __attribute__((ext_vector_type(2)));
 
 template <bool kFast>
 __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
@@ -191,13 +194,143 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
     }
 }
 
+// Fast arithmetic, packed: a 2-wave block per 16x16 tile; wave w owns rows 8w..8w+7 and each
+// lane owns the two pixels (x, y) and (x + 8, y) of its row, so every per-pixel operation
+// runs as one v_pk_* instruction on a float2 (CDNA4 reaches its fp32 rate only with packed
+// math).  A wave iterates over the splats that touch either of its two 8x8 quadrants.
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(128) void k_blend_fast2(const GsrBlendArgs a) {
+    __shared__ float4 s_geo[kBatch];   // x, y, prescaled conic a, b
+    __shared__ float4 s_opc[kBatch];   // prescaled conic c, opacity, r, g
+    __shared__ float s_blue[kBatch];
+    __shared__ uint8_t s_mask[kBatch];
+    __shared__ uint8_t s_list[2][kBatch];
+
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t tx = blockIdx.x, ty_local = blockIdx.y, ty = a.row_begin + ty_local;
+    const int tx0 = (int)tx * GSR_TILE_X, ty0 = (int)ty * GSR_TILE_Y;
+    const int pxa = tx0 + (lane & 7), pxb = pxa + 8, py = ty0 + w * 8 + (lane >> 3);
+    const bool in_a = pxa < a.W && py < a.H, in_b = pxb < a.W && py < a.H;
+    bool done_a = !in_a, done_b = !in_b;
+    const v2f pfx = {(float)pxa, (float)pxb};
+    const float pfy = (float)py;
+
+    const uint2 range = a.ranges[ty_local * a.grid_x + tx];
+    v2f T = {1.0f, 1.0f}, C0 = {0.0f, 0.0f}, C1 = {0.0f, 0.0f}, C2 = {0.0f, 0.0f};
+    uint32_t last_a = 0, last_b = 0;
+    const float kL2e = 1.4426950408889634f;
+
+    for (uint32_t start = range.x; start < range.y; start += kBatch) {
+        if (__syncthreads_count(done_a && done_b) == 128) break;
+        for (int t = tid; t < kBatch; t += 128) {
+            const uint32_t idx = start + t;
+            if (idx >= range.y) break;
+            const SplatRecord r = a.records[a.point_list[idx]];
+            uint32_t m = 0xF;
+            if (a.cull) {
+                const float x = r.a.x, y = r.a.y, A = r.a.z, B = r.a.w, C = r.b.x;
+                const float ex = r.c.y, ey = r.c.z, twoL = 2.0f * r.c.w;
+                const float X0 = (float)tx0, Y0 = (float)ty0;
+                m = (uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0, X0 + 7, Y0, Y0 + 7) |
+                    ((uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0 + 8, X0 + 15, Y0, Y0 + 7) << 1) |
+                    ((uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0, X0 + 7, Y0 + 8, Y0 + 15) << 2) |
+                    ((uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0 + 8, X0 + 15, Y0 + 8, Y0 + 15) << 3);
+            }
+            s_geo[t] = make_float4(r.a.x, r.a.y, r.a.z * (-0.5f * kL2e), r.a.w * (-kL2e));
+            s_opc[t] = make_float4(r.b.x * (-0.5f * kL2e), r.b.y, r.b.z, r.b.w);
+            s_blue[t] = r.c.x;
+            s_mask[t] = (uint8_t)m;
+        }
+        __syncthreads();
+        const int n = (int)min((uint32_t)kBatch, range.y - start);
+
+        int count = 0;
+        for (int base = 0; base < n; base += 64) {
+            const int j = base + lane;
+            const bool keep = j < n && ((s_mask[j] >> (2 * w)) & 3u);
+            const uint64_t bal = __ballot(keep);
+            const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+            if (keep) s_list[w][count + __popcll(bal & lt)] = (uint8_t)j;
+            count += __popcll(bal);
+        }
+        if (count == 0 || __ballot(!(done_a && done_b)) == 0ull) continue;
+
+        int j = s_list[w][0];
+        float4 g = s_geo[j], q = s_opc[j];
+        float blue = s_blue[j];
+        for (int k = 0; k < count; ++k) {
+            const int jn = s_list[w][k + 1 < count ? k + 1 : k];
+            const float4 g_next = s_geo[jn], q_next = s_opc[jn];
+            const float blue_next = s_blue[jn];
+            const v2f dx = (v2f)g.x - pfx;
+            const float dy = g.y - pfy;
+            const v2f ady = __builtin_elementwise_fma((v2f)g.z, dx, (v2f)(g.w * dy));
+            const v2f p2 = __builtin_elementwise_fma(dx, ady, (v2f)(q.x * dy * dy));
+            v2f e;
+            e.x = __builtin_amdgcn_exp2f(p2.x);
+            e.y = __builtin_amdgcn_exp2f(p2.y);
+            const v2f oe = (v2f)q.y * e;
+            v2f alpha;
+            alpha.x = fminf(0.99f, oe.x);
+            alpha.y = fminf(0.99f, oe.y);
+            const v2f test_T = T * ((v2f)1.0f - alpha);
+            const bool live_a = !done_a && !(p2.x > 0.0f) && !(alpha.x < 1.0f / 255.0f);
+            const bool live_b = !done_b && !(p2.y > 0.0f) && !(alpha.y < 1.0f / 255.0f);
+            const bool acc_a = live_a && !(test_T.x < 0.0001f);
+            const bool acc_b = live_b && !(test_T.y < 0.0001f);
+            const v2f aT = alpha * T;
+            v2f wgt;
+            wgt.x = acc_a ? aT.x : 0.0f;
+            wgt.y = acc_b ? aT.y : 0.0f;
+            C0 = __builtin_elementwise_fma((v2f)q.z, wgt, C0);
+            C1 = __builtin_elementwise_fma((v2f)q.w, wgt, C1);
+            C2 = __builtin_elementwise_fma((v2f)blue, wgt, C2);
+            T.x = acc_a ? test_T.x : T.x;
+            T.y = acc_b ? test_T.y : T.y;
+            const uint32_t pos = start - range.x + (uint32_t)j + 1u;
+            last_a = acc_a ? pos : last_a;
+            last_b = acc_b ? pos : last_b;
+            done_a = done_a || (live_a && (test_T.x < 0.0001f));
+            done_b = done_b || (live_b && (test_T.y < 0.0001f));
+            j = jn;
+            g = g_next;
+            q = q_next;
+            blue = blue_next;
+            if ((k & 15) == 15 && __ballot(!(done_a && done_b)) == 0ull) break;
+        }
+    }
+
+    const int row = py - a.y0;
+    const size_t plane = (size_t)a.rows_out * a.W;
+    if (in_a) {
+        const size_t pid = (size_t)row * a.W + pxa;
+        if (a.final_T) a.final_T[pid] = T.x;
+        if (a.n_contrib) a.n_contrib[pid] = last_a;
+        a.out_color[pid] = C0.x + T.x * a.bg[0];
+        a.out_color[plane + pid] = C1.x + T.x * a.bg[1];
+        a.out_color[2 * plane + pid] = C2.x + T.x * a.bg[2];
+    }
+    if (in_b) {
+        const size_t pid = (size_t)row * a.W + pxb;
+        if (a.final_T) a.final_T[pid] = T.y;
+        if (a.n_contrib) a.n_contrib[pid] = last_b;
+        a.out_color[pid] = C0.y + T.y * a.bg[0];
+        a.out_color[plane + pid] = C1.y + T.y * a.bg[1];
+        a.out_color[2 * plane + pid] = C2.y + T.y * a.bg[2];
+    }
+}
+
 }  // namespace
 
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s) {
     if (a.rows_tiles == 0 || a.grid_x == 0) return hipSuccess;
-    if (a.fast)
-        hipLaunchKernelGGL(k_blend<true>, dim3(a.grid_x, a.rows_tiles), dim3(256), 0, s, a);
+    const dim3 grid(a.grid_x, a.rows_tiles);
+    if (a.fast == 2)
+        hipLaunchKernelGGL(k_blend_fast2, grid, dim3(128), 0, s, a);
+    else if (a.fast)
+        hipLaunchKernelGGL((k_blend<true>), grid, dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL(k_blend<false>, dim3(a.grid_x, a.rows_tiles), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_blend<false>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }

@@ -291,6 +291,6 @@ struct GsrBlendArgs {
     float *out_color, *final_T;
     uint32_t *n_contrib;
     int cull;
-    int fast;  // 1: folded-constant FMA arithmetic + raw v_exp_f32 (see blend.hip)
+    int fast;   // 1: folded-constant FMA arithmetic + raw v_exp_f32; 2: same, packed 2 px/lane
 };
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s);

@@ -141,7 +141,7 @@ const char *gsr_stage_name(int i);
  *   GSR_OPT_BLEND_FAST (default 1): blend arithmetic with log2(e) folded into the conic, FMA
  *     contraction and the hardware exp2; changes pixels by float rounding only (tolerance in
  *     tests/gpu_helpers.py).  0 keeps upstream's per-pixel operation order (IEEE, no FMA,
- *     ocml expf). */
+ *     ocml expf).  2 = the fast arithmetic with two pixels per lane in packed float2 math. */
 /*   GSR_OPT_SORT_ONESWEEP (default 0): 1 = one-kernel-per-pass radix sort with decoupled
  *     look-back; 0 = reduce-then-scan (identical results; faster on MI355X at these sizes,
  *     see DESIGN.md). */

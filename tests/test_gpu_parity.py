@@ -116,7 +116,7 @@ def test_empty_and_fully_culled(gpu, oracle_mod):
     assert np.all(hip["color"][1] == np.float32(0.2))
 
 
-@pytest.mark.parametrize("fast", [0, 1])
+@pytest.mark.parametrize("fast", [0, 1, 2])
 @pytest.mark.parametrize("scene", ["dense_720p", "elongated_close"])
 def test_cull_is_exact(gpu, fast, scene):
     """The blend's ellipse-vs-quadrant cull changes nothing: bit-identical image either way,
@@ -144,14 +144,20 @@ def test_cull_is_exact(gpu, fast, scene):
         np.testing.assert_array_equal(on[k].view(np.uint32), off[k].view(np.uint32), err_msg=k)
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("name", ["C1_10k_640x480_sh3", "C2_100k_1080p_sh0",
                                   "inside_cloud_20k_1160x522_sh3"])
-def test_exact_blend_parity(gpu, oracle_mod, exact_blend, name):
-    """GSR_OPT_BLEND_FAST = 0 (upstream operation order): binning bit-exact, image within the
-    stated tolerance (in practice >= 92 % of pixels bit-equal; only expf differs)."""
+def test_blend_mode_parity(gpu, oracle_mod, name, mode):
+    """Every blend arithmetic mode (GSR_OPT_BLEND_FAST: 0 = upstream operation order, 1 = fused,
+    2 = fused + packed two pixels per lane): binning bit-exact, image within the tolerance."""
     P, W, H, deg, seed, eye = CASES[name]
     s = scene_inputs(synthetic_gaussians(P, deg, seed), static_camera(W, H, eye), deg)
-    assert_parity(run_hip(s, gpu), run_oracle(oracle_mod, s))
+    _set_option(gpu, _lib.GSR_OPT_BLEND_FAST, mode)
+    try:
+        hip = run_hip(s, gpu)
+    finally:
+        _set_option(gpu, _lib.GSR_OPT_BLEND_FAST, 1)
+    assert_parity(hip, run_oracle(oracle_mod, s))
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])
@@ -200,7 +206,7 @@ def c3_oracle(oracle_mod):
     return s, run_oracle(oracle_mod, s)
 
 
-@pytest.mark.parametrize("fast", [0, 1])
+@pytest.mark.parametrize("fast", [0, 1, 2])
 def test_headline_config_c3(gpu, c3_oracle, fast):
     """Config C3 at full size: 1M Gaussians, 1920x1080, SH degree 3, static camera."""
     s, orc = c3_oracle
