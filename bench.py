@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sort-shape", type=int, default=None, help="GSR_OPT_TILE_SORT_SHAPE (tuning)")
     ap.add_argument("--onesweep", action="store_true", help="GSR_OPT_SORT_ONESWEEP (tuning)")
+    ap.add_argument("--unfused", action="store_true", help="GSR_OPT_FUSED_BINNING=0 (tuning)")
     ap.add_argument("--blend", default="fast", choices=["exact", "fast", "packed"],
                     help="blend arithmetic: GSR_OPT_BLEND_FAST (default) or upstream's exact "
                          "operation order")
@@ -158,6 +159,8 @@ def main():
                "gsr_set_option")
     if args.sort_shape is not None:
         _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_TILE_SORT_SHAPE, args.sort_shape), "opt")
+    if args.unfused:
+        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_FUSED_BINNING, 0), "opt")
     if args.onesweep:
         _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_SORT_ONESWEEP, 1), "opt")
 

@@ -17,6 +17,7 @@ GSR_OPT_BLEND_CULL = 1
 GSR_OPT_BLEND_FAST = 2
 GSR_OPT_SORT_ONESWEEP = 3
 GSR_OPT_TILE_SORT_SHAPE = 4
+GSR_OPT_FUSED_BINNING = 5
 
 # Symbols include/gsr.h declares (checked by the CPU test suite).
 EXPORTED_SYMBOLS = (

@@ -42,8 +42,8 @@ const char *kStageNames[kStages] = {"preprocess", "depth_sort", "scan",  "duplic
 struct gsr_context {
     int device = 0;
     // per-Gaussian workspace
-    DevBuf records, strip_tiles, sort_keys, sort_vals, sort_keys_alt, sort_vals_alt, partials,
-        total, hist, digit_total, offsets, chunk_first;
+    DevBuf records, strip_rect, sort_keys, sort_vals, sort_keys_alt, sort_vals_alt, partials,
+        total, hist, digit_total, bin, chunk_first;
     // onesweep sort state: [0,1024) depth-sort digit counts, [1024,2048) tile-sort counts,
     // then the ticket word; look-back granules
     DevBuf sort_ctl, status;
@@ -62,6 +62,7 @@ struct gsr_context {
     int fast = 1;
     int onesweep = 0;
     int tile_sort_shape = 3;  // 8 waves x 8 keys/lane: fastest measured
+    int fused_binning = 1;    // duplicate fused with the first tile-sort pass
     // Stage timing: a ring of event sets, one per forward, read back after the timed region.
     bool timing = false;
     int64_t timed_frames = 0;
@@ -110,7 +111,7 @@ int grow_zeroed(gsr_context *ctx, DevBuf &b, size_t bytes, hipStream_t s) {
 int reserve_P(gsr_context *ctx, int64_t P, hipStream_t s) {
     const size_t n = (size_t)std::max<int64_t>(P, 1);
     GSR_TRY(grow(ctx, ctx->records, n * sizeof(gsr::SplatRecord), s));
-    GSR_TRY(grow(ctx, ctx->strip_tiles, n * 4, s));
+    GSR_TRY(grow(ctx, ctx->strip_rect, n * 8, s));
     GSR_TRY(grow(ctx, ctx->sort_keys, n * 4, s));
     GSR_TRY(grow(ctx, ctx->sort_vals, n * 4, s));
     GSR_TRY(grow(ctx, ctx->sort_keys_alt, n * 4, s));
@@ -119,7 +120,7 @@ int reserve_P(gsr_context *ctx, int64_t P, hipStream_t s) {
     GSR_TRY(grow_zeroed(ctx, ctx->total, 16, s));  // [K (u64), look-back error flag (u32)]
     GSR_TRY(grow(ctx, ctx->hist, (size_t)gsr_radix_hist_words(P) * 4, s));
     GSR_TRY(grow(ctx, ctx->digit_total, 256 * 4, s));
-    GSR_TRY(grow(ctx, ctx->offsets, n * 4, s));
+    GSR_TRY(grow(ctx, ctx->bin, n * 16, s));
     GSR_TRY(grow_zeroed(ctx, ctx->sort_ctl, 2048 * 4 + 256, s));
     GSR_TRY(grow_zeroed(ctx, ctx->status, (size_t)gsr_onesweep_status_words(P) * 8, s));
     return GSR_OK;
@@ -199,10 +200,10 @@ int gsr_create(gsr_context **out) {
 void gsr_destroy(gsr_context *ctx) {
     if (!ctx) return;
     (void)hipDeviceSynchronize();
-    DevBuf *bufs[] = {&ctx->records,       &ctx->strip_tiles,   &ctx->sort_keys,
+    DevBuf *bufs[] = {&ctx->records,       &ctx->strip_rect,    &ctx->sort_keys,
                       &ctx->sort_vals,     &ctx->sort_keys_alt, &ctx->sort_vals_alt,
                       &ctx->partials,      &ctx->total,         &ctx->hist,
-                      &ctx->digit_total,   &ctx->offsets,       &ctx->chunk_first,
+                      &ctx->digit_total,   &ctx->bin,           &ctx->chunk_first,
                       &ctx->sort_ctl,      &ctx->status,
                       &ctx->tile_keys,     &ctx->tile_vals,
                       &ctx->tile_keys_alt, &ctx->tile_vals_alt, &ctx->ranges_local};
@@ -236,6 +237,10 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
     }
     if (option == GSR_OPT_SORT_ONESWEEP) {
         ctx->onesweep = value ? 1 : 0;
+        return GSR_OK;
+    }
+    if (option == GSR_OPT_FUSED_BINNING) {
+        ctx->fused_binning = value ? 1 : 0;
         return GSR_OK;
     }
     if (option == GSR_OPT_TILE_SORT_SHAPE) {
@@ -307,6 +312,8 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
 
     const uint32_t gx = (uint32_t)((W + GSR_TILE_X - 1) / GSR_TILE_X);
     const uint32_t gy = (uint32_t)((H + GSR_TILE_Y - 1) / GSR_TILE_Y);
+    if (gx > 0xFFFFu || gy > 0xFFFFu)  // packed 16-bit tile rects (preprocess.hip)
+        return fail(GSR_E_INVALID, "gsr_forward: image larger than 65535 tiles per side");
     uint32_t rb = 0, re = gy;
     if (st->tile_row_begin != 0 || st->tile_row_end != 0) {
         if (st->tile_row_begin < 0 || st->tile_row_end > (int)gy ||
@@ -384,7 +391,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     pa.records = static_cast<gsr::SplatRecord *>(ctx->records.p);
     pa.sort_keys = static_cast<uint32_t *>(ctx->sort_keys.p);
     pa.sort_vals = static_cast<uint32_t *>(ctx->sort_vals.p);
-    pa.strip_tiles = static_cast<uint32_t *>(ctx->strip_tiles.p);
+    pa.strip_rect = static_cast<uint2 *>(ctx->strip_rect.p);
     pa.depths = out->depths;
     pa.means2D = out->means2D;
     pa.conic_opacity = out->conic_opacity;
@@ -418,7 +425,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     // ---- 3. offsets scan over depth-sorted strip tile counts; K readback --------------------
     uint32_t *partials = static_cast<uint32_t *>(ctx->partials.p);
     uint64_t *d_total = static_cast<uint64_t *>(ctx->total.p);
-    GSR_HIP(gsr_launch_scan_reduce(perm, pa.strip_tiles, P, partials, s), "scan launch");
+    GSR_HIP(gsr_launch_scan_reduce(perm, pa.strip_rect, P, partials, s), "scan launch");
     GSR_HIP(gsr_launch_scan_partials(partials, gsr_scan_blocks(P), d_total, s), "scan launch");
     GSR_HIP(hipMemcpyAsync(ctx->h_total, d_total, 16, hipMemcpyDeviceToHost, s),
             "hipMemcpyAsync(num_rendered)");
@@ -437,19 +444,31 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     uint32_t *tv = static_cast<uint32_t *>(ctx->tile_vals.p);
     uint32_t *tk_alt = static_cast<uint32_t *>(ctx->tile_keys_alt.p);
     uint32_t *tv_alt = static_cast<uint32_t *>(ctx->tile_vals_alt.p);
-    uint32_t *offsets = static_cast<uint32_t *>(ctx->offsets.p);
+    uint4 *bin = static_cast<uint4 *>(ctx->bin.p);
     uint32_t *chunk_first = static_cast<uint32_t *>(ctx->chunk_first.p);
     hist = static_cast<uint32_t *>(ctx->hist.p);  // may have been regrown
+    const GsrRadixPlan tplan = gsr_radix_plan(0, tbits);
+    const bool fused = !ctx->onesweep && ctx->fused_binning;
     if (K > 0) {
-        GSR_HIP(gsr_launch_scan_down(perm, pa.strip_tiles, partials, P, d_total, offsets,
-                                     chunk_first, s),
+        GSR_HIP(gsr_launch_scan_down(perm, pa.strip_rect, partials, P, d_total, bin, chunk_first,
+                                     s),
                 "scan_down launch");
-        // the onesweep tile sort takes its digit counts from the duplicate (fused)
-        GSR_HIP(gsr_launch_duplicate(perm, offsets, chunk_first, (int64_t)K, pa.records,
-                                     out->radii, gx, gy, rb, tk, tv,
-                                     ctx->onesweep ? gsr_radix_plan(0, tbits) : GsrRadixPlan{},
-                                     onesweep_ws(ctx, 1).ghist, s),
-                "duplicate launch");
+        if (fused) {
+            // duplicate fused with the first tile-sort pass (a single pass when tbits == 0)
+            GSR_HIP(gsr_launch_dup_sort_pass(bin, chunk_first, (int64_t)K, gx,
+                                             tplan.n ? tplan.shift[0] : 0,
+                                             tplan.n ? tplan.nbits[0] : 0, hist, digit_total,
+                                             tk_alt, tv_alt, s),
+                    "duplicate launch");
+            std::swap(tk, tk_alt);
+            std::swap(tv, tv_alt);
+        } else {
+            // the onesweep tile sort takes its digit counts from the duplicate (fused)
+            GSR_HIP(gsr_launch_duplicate(bin, chunk_first, (int64_t)K, gx, tk, tv,
+                                         ctx->onesweep ? tplan : GsrRadixPlan{},
+                                         onesweep_ws(ctx, 1).ghist, s),
+                    "duplicate launch");
+        }
     }
     GSR_TRY(stage_end(3));
 
@@ -460,7 +479,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
                 "tile sort launch");
     } else {
         GSR_HIP(gsr_radix_sort_pairs(&tk, &tv, &tk_alt, &tv_alt, (int64_t)K, 0, tbits, hist,
-                                     digit_total, s, ctx->tile_sort_shape),
+                                     digit_total, s, ctx->tile_sort_shape, fused ? 1 : 0),
                 "tile sort launch");
     }
     GSR_TRY(stage_end(4));

@@ -9,7 +9,7 @@
 // by Gaussian index, exactly as upstream's stable 64-bit sort orders it, so point lists and
 // ranges are bit-identical while the K-sized sort moves 8-B pairs over 2 passes instead of
 // 12-B pairs over 6.
-#include "gsr_internal.h"
+#include "radix_tile.h"
 
 using namespace gsr;
 
@@ -21,8 +21,10 @@ constexpr int kTile = kBlock * kItems;  // 1024 depth-sorted Gaussians per scan 
 constexpr uint32_t kChunk = 2048;        // output pairs per duplicate block
 
 // Pass 1 of the scan: per-block sum of the strip tile counts, gathered in depth order.
+__device__ __forceinline__ uint32_t rect_count(uint2 r) { return (r.x >> 16) * (r.y >> 16); }
+
 __global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t *__restrict__ perm,
-                                                        const uint32_t *__restrict__ strip_tiles,
+                                                        const uint2 *__restrict__ strip_rect,
                                                         int64_t n, uint32_t *__restrict__ partials) {
     __shared__ uint32_t s_tmp[4];
     const int64_t base = (int64_t)blockIdx.x * kTile;
@@ -30,7 +32,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t *__restri
 #pragma unroll 4
     for (int j = 0; j < kItems; ++j) {
         const int64_t e = base + j * kBlock + threadIdx.x;
-        if (e < n) sum += strip_tiles[perm[e]];
+        if (e < n) sum += rect_count(strip_rect[perm[e]]);
     }
     uint32_t total;
     block256_exclusive_scan(sum, s_tmp, total);
@@ -54,24 +56,29 @@ __global__ __launch_bounds__(kBlock) void k_scan_partials(uint32_t *__restrict__
     if (threadIdx.x == 0) *total = carry;
 }
 
-// Pass 3: exclusive offsets of the depth-sorted Gaussians (offsets[e]) and, for every chunk of
+// Pass 3: exclusive offsets of the depth-sorted Gaussians, written with everything the
+// duplication needs as bin[e] = {offset, id, x0 | width << 16, strip-local row0} (coalesced,
+// so the duplicate kernels stage their Gaussians without a gather), and, for every chunk of
 // kChunk output pairs, the first Gaussian whose pairs reach into it (chunk_first[c]);
 // chunk_first[n_chunks] = one past the last Gaussian with pairs.  Gaussians without pairs in
 // the strip carry the sentinel depth key, so they all sit after the last non-empty one.
 __global__ __launch_bounds__(kBlock) void k_scan_down(const uint32_t *__restrict__ perm,
-                                                      const uint32_t *__restrict__ strip_tiles,
+                                                      const uint2 *__restrict__ strip_rect,
                                                       const uint32_t *__restrict__ partials,
                                                       int64_t n, const uint64_t *__restrict__ total,
-                                                      uint32_t *__restrict__ offsets,
+                                                      uint4 *__restrict__ bin,
                                                       uint32_t *__restrict__ chunk_first) {
     __shared__ uint32_t s_tmp[4];
     const int tid = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)tid * kItems;
-    uint32_t cnt[kItems], sum = 0;
+    uint32_t cnt[kItems], id[kItems], sum = 0;
+    uint2 rc[kItems];
 #pragma unroll
     for (int j = 0; j < kItems; ++j) {
         const int64_t e = base + j;
-        cnt[j] = e < n ? strip_tiles[perm[e]] : 0u;
+        id[j] = e < n ? perm[e] : 0u;
+        rc[j] = e < n ? strip_rect[id[j]] : make_uint2(0u, 0u);
+        cnt[j] = rect_count(rc[j]);
         sum += cnt[j];
     }
     uint32_t blk_total;
@@ -82,8 +89,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_down(const uint32_t *__restrict
     for (int j = 0; j < kItems; ++j) {
         const int64_t e = base + j;
         if (e >= n) break;
-        offsets[e] = off;
         if (cnt[j]) {
+            bin[e] = make_uint4(off, id[j], rc[j].x, rc[j].y & 0xFFFFu);
             for (uint32_t c = (off + kChunk - 1) / kChunk; c * kChunk < off + cnt[j]; ++c)
                 chunk_first[c] = (uint32_t)e;
             if (off + cnt[j] == K) chunk_first[n_chunks] = (uint32_t)e + 1u;
@@ -97,12 +104,9 @@ __global__ __launch_bounds__(kBlock) void k_scan_down(const uint32_t *__restrict
 // id), row-major over each Gaussian's rect like upstream.  The Gaussians overlapping the
 // chunk are staged in LDS; each output finds its owner by binary search over their offsets.
 __global__ __launch_bounds__(kBlock) void k_duplicate(
-    const uint32_t *__restrict__ perm, const uint32_t *__restrict__ offsets,
-    const uint32_t *__restrict__ chunk_first, uint32_t K, uint32_t n_chunks,
-    const SplatRecord *__restrict__ records, const int32_t *__restrict__ radii, uint32_t gx,
-    uint32_t gy, uint32_t row_begin,
-    uint32_t *__restrict__ tile_keys, uint32_t *__restrict__ tile_vals, const GsrRadixPlan plan,
-    uint32_t *__restrict__ ghist) {
+    const uint4 *__restrict__ bin, const uint32_t *__restrict__ chunk_first, uint32_t K,
+    uint32_t n_chunks, uint32_t gx, uint32_t *__restrict__ tile_keys,
+    uint32_t *__restrict__ tile_vals, const GsrRadixPlan plan, uint32_t *__restrict__ ghist) {
     __shared__ uint32_t s_hist[GSR_RADIX_MAX_PASSES][256];  // digit counts of the tile sort
     __shared__ uint32_t s_off[kChunk + 1];
     __shared__ uint32_t s_id[kChunk + 1];
@@ -116,13 +120,11 @@ __global__ __launch_bounds__(kBlock) void k_duplicate(
     const int ne = (int)(e1 - e0);  // <= kChunk + 1: every staged Gaussian owns >= 1 pair
     for (int i = tid; i < GSR_RADIX_MAX_PASSES * 256; i += kBlock) (&s_hist[0][0])[i] = 0;
     for (int i = tid; i < ne; i += kBlock) {
-        const uint32_t id = perm[e0 + i];
-        const float4 ra = records[id].a;
-        const Rect rc = get_rect(ra.x, ra.y, radii[id], gx, gy);
-        s_off[i] = offsets[e0 + i];
-        s_id[i] = id;
-        s_x0w[i] = rc.x0 | ((rc.x1 - rc.x0) << 16);
-        s_row0[i] = (max(rc.y0, row_begin) - row_begin) * gx;
+        const uint4 b = bin[e0 + i];
+        s_off[i] = b.x;
+        s_id[i] = b.y;
+        s_x0w[i] = b.z;
+        s_row0[i] = b.w * gx;
     }
     __syncthreads();
     const uint32_t o_end = min(K, (c + 1) * kChunk);
@@ -150,6 +152,200 @@ __global__ __launch_bounds__(kBlock) void k_duplicate(
         const uint32_t c = (&s_hist[0][0])[i];
         if (c) atomicAdd(&ghist[i], c);
     }
+}
+
+// ---- fused duplicate + first tile-sort pass ------------------------------------------------
+// The tile sort's first radix pass needs, per sort tile, the digit histogram of its pairs and
+// then the pairs themselves in order.  Both are regenerated here from the depth-sorted
+// Gaussians instead of being written by k_duplicate and read back: k_dup_count builds the
+// histogram of each 4096-pair output chunk (= one sort tile), k_rs_scan scans it, and
+// k_dup_scatter regenerates the chunk in registers, ranks it by the digit and scatters it --
+// the K-sized pair array is written once and never read by this pass.
+constexpr int kFW = 8, kFIt = 8;                   // 8 waves x 8 pairs per lane
+constexpr uint32_t kFChunk = kFW * 64 * kFIt;      // 4096 = 2 duplicate chunks
+static_assert(kFChunk == 2 * kChunk, "fused chunks are pairs of scan_down chunks");
+
+constexpr int kStageCap = 2048;  // Gaussians staged in LDS; denser chunks read global memory
+
+struct DupStage {
+    uint32_t off[kStageCap];
+    uint32_t id[kStageCap];
+    uint32_t x0w[kStageCap];   // rect x0 | width << 16
+    uint32_t row0[kStageCap];  // first strip-local tile row * gx
+};
+
+struct GaussRange {
+    uint32_t e0;
+    int ne;  // <= kFChunk + 1: every Gaussian of the range owns >= 1 pair
+};
+
+// The Gaussians whose pairs overlap fused chunk c.  n_chunks = scan_down chunk count.
+__device__ __forceinline__ GaussRange fused_chunk_range(uint32_t c,
+                                                        const uint32_t *__restrict__ chunk_first,
+                                                        uint32_t n_chunks) {
+    const uint32_t e_end_all = chunk_first[n_chunks];
+    const uint32_t e0 = chunk_first[2 * c];
+    const uint32_t e1 =
+        (2 * c + 2 < n_chunks) ? min(chunk_first[2 * c + 2] + 1u, e_end_all) : e_end_all;
+    return {e0, (int)(e1 - e0)};
+}
+
+struct BinSrc {
+    const uint4 *bin;
+    uint32_t gx;
+    __device__ __forceinline__ void info(uint32_t e, uint32_t &id, uint32_t &x0w,
+                                         uint32_t &row0) const {
+        const uint4 b = bin[e];
+        id = b.y;
+        x0w = b.z;
+        row0 = b.w * gx;
+    }
+};
+
+// Stage the range in LDS if it fits (block-uniform decision).
+__device__ __forceinline__ bool stage_range(const GaussRange &r, const BinSrc &src,
+                                            DupStage &st) {
+    if (r.ne > kStageCap) return false;
+    for (int i = threadIdx.x; i < r.ne; i += kFW * 64) {
+        const uint4 b = src.bin[r.e0 + i];
+        st.off[i] = b.x;
+        st.id[i] = b.y;
+        st.x0w[i] = b.z;
+        st.row0[i] = b.w * src.gx;
+    }
+    return true;
+}
+
+// Pairs [o0, o0 + kFIt) of the output, row-major over each Gaussian's rect (upstream
+// duplicateWithKeys order); outputs >= o_end get the sentinel key 0xFFFFFFFF.  Reads the
+// staged copy, or global memory when the range did not fit.
+__device__ __forceinline__ void gen_pairs(const DupStage &st, bool staged, const GaussRange &r,
+                                          const BinSrc &src, uint32_t o0, uint32_t o_end,
+                                          uint32_t (&kk)[kFIt], uint32_t (&vv)[kFIt]) {
+#pragma unroll
+    for (int j = 0; j < kFIt; ++j) {
+        kk[j] = 0xFFFFFFFFu;
+        vv[j] = 0u;
+    }
+    if (o0 >= o_end) return;
+    const uint4 *bins = src.bin + r.e0;
+    auto off_at = [&](int i) { return staged ? st.off[i] : bins[i].x; };
+    auto info_at = [&](int i, uint32_t &id, uint32_t &x0w, uint32_t &row0) {
+        if (staged) {
+            id = st.id[i];
+            x0w = st.x0w[i];
+            row0 = st.row0[i];
+        } else {
+            src.info(r.e0 + i, id, x0w, row0);
+        }
+    };
+    const int ne = r.ne;
+    int lo = 0, hi = ne - 1;  // last Gaussian of the range whose offset <= o0
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off_at(mid) <= o0) lo = mid;
+        else hi = mid - 1;
+    }
+    uint32_t nxt = lo + 1 < ne ? off_at(lo + 1) : 0xFFFFFFFFu;
+    uint32_t id, x0w, row0;
+    info_at(lo, id, x0w, row0);
+    uint32_t width = x0w >> 16;
+    const uint32_t local = o0 - off_at(lo);
+    const uint32_t row = local / width;
+    uint32_t col = local - row * width;
+    uint32_t rowkey = row0 + row * src.gx + (x0w & 0xFFFFu);
+#pragma unroll
+    for (int j = 0; j < kFIt; ++j) {
+        const uint32_t o = o0 + (uint32_t)j;
+        if (o < o_end) {
+            if (o == nxt) {  // next Gaussian (each owns >= 1 pair)
+                ++lo;
+                nxt = lo + 1 < ne ? off_at(lo + 1) : 0xFFFFFFFFu;
+                info_at(lo, id, x0w, row0);
+                width = x0w >> 16;
+                col = 0;
+                rowkey = row0 + (x0w & 0xFFFFu);
+            }
+            kk[j] = rowkey + col;
+            vv[j] = id;
+            if (++col == width) {
+                col = 0;
+                rowkey += src.gx;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kFW * 64) void k_dup_count(
+    const uint4 *__restrict__ bin, const uint32_t *__restrict__ chunk_first, uint32_t K,
+    uint32_t n_chunks, uint32_t gx, int shift, uint32_t mask, uint32_t *__restrict__ hist,
+    int64_t nb) {
+    __shared__ DupStage st;
+    __shared__ uint32_t s_h[kFW][kRadixBins];
+    const int tid = threadIdx.x, w = tid >> 6;
+    const uint32_t c = blockIdx.x;
+    for (int i = tid; i < kFW * kRadixBins; i += kFW * 64) (&s_h[0][0])[i] = 0;
+    const BinSrc src{bin, gx};
+    const GaussRange r = fused_chunk_range(c, chunk_first, n_chunks);
+    const bool staged = stage_range(r, src, st);
+    __syncthreads();
+    uint32_t kk[kFIt], vv[kFIt];
+    gen_pairs(st, staged, r, src, c * kFChunk + (uint32_t)tid * kFIt, min(K, (c + 1) * kFChunk),
+              kk, vv);
+#pragma unroll
+    for (int j = 0; j < kFIt; ++j)
+        if (kk[j] != 0xFFFFFFFFu) atomicAdd(&s_h[w][(kk[j] >> shift) & mask], 1u);
+    __syncthreads();
+    if (tid < kRadixBins) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int i = 0; i < kFW; ++i) t += s_h[i][tid];
+        hist[(int64_t)tid * nb + c] = t;
+    }
+}
+
+__global__ __launch_bounds__(kFW * 64) void k_dup_scatter(
+    const uint4 *__restrict__ bin, const uint32_t *__restrict__ chunk_first, uint32_t K,
+    uint32_t n_chunks, uint32_t gx, int shift, int nbits, const uint32_t *__restrict__ hist,
+    int64_t nb, const uint32_t *__restrict__ digit_total, uint32_t *__restrict__ keys_out,
+    uint32_t *__restrict__ vals_out) {
+    union alignas(16) Smem {
+        DupStage st;
+        struct {
+            uint32_t keys[kFChunk];
+            uint32_t vals[kFChunk];
+        } kv;
+    };
+    __shared__ Smem u;
+    __shared__ RadixTileSmem<kFW, kFIt> sm;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t c = blockIdx.x;
+    const BinSrc src{bin, gx};
+    const GaussRange r = fused_chunk_range(c, chunk_first, n_chunks);
+    const bool staged = stage_range(r, src, u.st);
+    __syncthreads();
+    uint32_t kk[kFIt], vv[kFIt];
+    const uint32_t o_end = min(K, (c + 1) * kFChunk);
+    gen_pairs(u.st, staged, r, src, c * kFChunk + (uint32_t)tid * kFIt, o_end, kk, vv);
+    __syncthreads();
+    // blocked (thread-consecutive) -> wave-striped layout through LDS
+    static_assert(kFIt == 8, "two 16-B LDS writes per array");
+    uint4 *k4 = reinterpret_cast<uint4 *>(u.kv.keys) + tid * 2;
+    uint4 *v4 = reinterpret_cast<uint4 *>(u.kv.vals) + tid * 2;
+    k4[0] = make_uint4(kk[0], kk[1], kk[2], kk[3]);
+    k4[1] = make_uint4(kk[4], kk[5], kk[6], kk[7]);
+    v4[0] = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+    v4[1] = make_uint4(vv[4], vv[5], vv[6], vv[7]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kFIt; ++j) {
+        const int e = w * (kFChunk / kFW) + j * 64 + lane;
+        kk[j] = u.kv.keys[e];
+        vv[j] = u.kv.vals[e];
+    }
+    // (radix_tile_scatter's first barrier orders these reads before its LDS writes)
+    radix_tile_scatter<kFW, kFIt>(kk, vv, (int)(o_end - c * kFChunk), shift, nbits, hist, nb, c,
+                                  digit_total, keys_out, vals_out, sm, u.kv.keys, u.kv.vals);
 }
 
 // upstream identifyTileRanges over the tile-sorted keys (ranges pre-zeroed).
@@ -180,11 +376,11 @@ __global__ __launch_bounds__(kBlock) void k_globalize(const uint32_t *__restrict
 
 int64_t gsr_scan_blocks(int64_t n) { return (n + kTile - 1) / kTile; }
 
-hipError_t gsr_launch_scan_reduce(const uint32_t *perm, const uint32_t *strip_tiles, int64_t n,
+hipError_t gsr_launch_scan_reduce(const uint32_t *perm, const uint2 *strip_rect, int64_t n,
                                   uint32_t *partials, hipStream_t s) {
     const int64_t nb = gsr_scan_blocks(n);
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(kBlock), 0, s, perm, strip_tiles, n,
+    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(kBlock), 0, s, perm, strip_rect, n,
                        partials);
     return hipGetLastError();
 }
@@ -195,28 +391,45 @@ hipError_t gsr_launch_scan_partials(uint32_t *partials, int64_t nb, uint64_t *to
     return hipGetLastError();
 }
 
-hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint32_t *strip_tiles,
+hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint2 *strip_rect,
                                 const uint32_t *partials, int64_t n, const uint64_t *total,
-                                uint32_t *offsets, uint32_t *chunk_first, hipStream_t s) {
+                                uint4 *bin, uint32_t *chunk_first, hipStream_t s) {
     const int64_t nb = gsr_scan_blocks(n);
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_scan_down, dim3((unsigned)nb), dim3(kBlock), 0, s, perm, strip_tiles,
-                       partials, n, total, offsets, chunk_first);
+    hipLaunchKernelGGL(k_scan_down, dim3((unsigned)nb), dim3(kBlock), 0, s, perm, strip_rect,
+                       partials, n, total, bin, chunk_first);
     return hipGetLastError();
 }
 
 int64_t gsr_duplicate_chunks(int64_t K) { return (K + kChunk - 1) / kChunk; }
 
-hipError_t gsr_launch_duplicate(const uint32_t *perm, const uint32_t *offsets,
-                                const uint32_t *chunk_first, int64_t K, const SplatRecord *records,
-                                const int32_t *radii, uint32_t gx, uint32_t gy, uint32_t row_begin,
-                                uint32_t *tile_keys, uint32_t *tile_vals,
+hipError_t gsr_launch_duplicate(const uint4 *bin, const uint32_t *chunk_first, int64_t K,
+                                uint32_t gx, uint32_t *tile_keys, uint32_t *tile_vals,
                                 const GsrRadixPlan &plan, uint32_t *ghist, hipStream_t s) {
     const int64_t nc = gsr_duplicate_chunks(K);
     if (nc == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_duplicate, dim3((unsigned)nc), dim3(kBlock), 0, s, perm, offsets,
-                       chunk_first, (uint32_t)K, (uint32_t)nc, records, radii, gx, gy, row_begin,
-                       tile_keys, tile_vals, plan, ghist);
+    hipLaunchKernelGGL(k_duplicate, dim3((unsigned)nc), dim3(kBlock), 0, s, bin, chunk_first,
+                       (uint32_t)K, (uint32_t)nc, gx, tile_keys, tile_vals, plan, ghist);
+    return hipGetLastError();
+}
+
+int64_t gsr_fused_chunks(int64_t K) { return (K + kFChunk - 1) / kFChunk; }
+
+hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_first, int64_t K,
+                                    uint32_t gx, int shift, int nbits, uint32_t *hist,
+                                    uint32_t *digit_total, uint32_t *keys_out, uint32_t *vals_out,
+                                    hipStream_t s) {
+    const int64_t nb = gsr_fused_chunks(K);
+    if (nb == 0) return hipSuccess;
+    const uint32_t nc = (uint32_t)gsr_duplicate_chunks(K);
+    const uint32_t mask = (1u << nbits) - 1u;
+    hipLaunchKernelGGL(k_dup_count, dim3((unsigned)nb), dim3(kFW * 64), 0, s, bin, chunk_first,
+                       (uint32_t)K, nc, gx, shift, mask, hist, nb);
+    hipError_t e = gsr_launch_digit_scan(hist, nb, digit_total, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_dup_scatter, dim3((unsigned)nb), dim3(kFW * 64), 0, s, bin, chunk_first,
+                       (uint32_t)K, nc, gx, shift, nbits, hist, nb, digit_total, keys_out,
+                       vals_out);
     return hipGetLastError();
 }
 

@@ -209,7 +209,10 @@ struct GsrPreprocessArgs {
     // workspace outputs
     int32_t *radii;
     gsr::SplatRecord *records;
-    uint32_t *sort_keys, *sort_vals, *strip_tiles;
+    uint32_t *sort_keys, *sort_vals;
+    // per Gaussian: strip-clipped tile rect {x0 | width << 16, strip-local row0 | rows << 16},
+    // {0, 0} when it has no pair in the strip (grid dimensions < 2^16, checked by the host)
+    uint2 *strip_rect;
     // optional debug outputs
     float *depths, *means2D, *conic_opacity, *rgb;
     uint32_t *tiles_touched;
@@ -231,7 +234,10 @@ int64_t gsr_radix_hist_words(int64_t n);
 hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
                                 uint32_t **vals_alt, int64_t n, int begin_bit, int end_bit,
                                 uint32_t *hist, uint32_t *digit_total, hipStream_t s,
-                                int shape = 0);
+                                int shape = 0, int first_pass = 0);
+// k_rs_scan alone: per digit, exclusive scan of hist[d][0..nb) across tiles -> digit_total[d].
+hipError_t gsr_launch_digit_scan(uint32_t *hist, int64_t nb, uint32_t *digit_total,
+                                 hipStream_t s);
 
 // Onesweep radix sort (one kernel per pass, decoupled look-back).  Pass plan: the key bits
 // [begin, end) split into n <= 4 passes of <= 8 bits.  ghist holds the global digit counts of
@@ -261,20 +267,27 @@ hipError_t gsr_onesweep_sort(uint32_t **keys, uint32_t **vals, uint32_t **keys_a
 // Binning: offsets scan over depth-sorted strip tile counts, duplicate into (tile, id)
 // pairs, and tile ranges.
 int64_t gsr_scan_blocks(int64_t n);
-hipError_t gsr_launch_scan_reduce(const uint32_t *perm, const uint32_t *strip_tiles, int64_t n,
+hipError_t gsr_launch_scan_reduce(const uint32_t *perm, const uint2 *strip_rect, int64_t n,
                                   uint32_t *partials, hipStream_t s);
 hipError_t gsr_launch_scan_partials(uint32_t *partials, int64_t nb, uint64_t *total,
                                     hipStream_t s);
-hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint32_t *strip_tiles,
+// bin[e] (e = depth rank, only for Gaussians with pairs) = {exclusive pair offset, Gaussian
+// id, x0 | width << 16, strip-local row0}
+hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint2 *strip_rect,
                                 const uint32_t *partials, int64_t n, const uint64_t *total,
-                                uint32_t *offsets, uint32_t *chunk_first, hipStream_t s);
+                                uint4 *bin, uint32_t *chunk_first, hipStream_t s);
 int64_t gsr_duplicate_chunks(int64_t K);
-hipError_t gsr_launch_duplicate(const uint32_t *perm, const uint32_t *offsets,
-                                const uint32_t *chunk_first, int64_t K,
-                                const gsr::SplatRecord *records, const int32_t *radii,
-                                uint32_t gx, uint32_t gy,
-                                uint32_t row_begin, uint32_t *tile_keys, uint32_t *tile_vals,
+hipError_t gsr_launch_duplicate(const uint4 *bin, const uint32_t *chunk_first, int64_t K,
+                                uint32_t gx, uint32_t *tile_keys, uint32_t *tile_vals,
                                 const GsrRadixPlan &plan, uint32_t *ghist, hipStream_t s);
+// Fused duplicate + first tile-sort radix pass (digit (key >> shift) & (2^nbits - 1)):
+// writes the K pairs, stably ordered by that digit, to keys_out / vals_out.  Uses
+// chunk_first as written by gsr_launch_scan_down; hist needs gsr_radix_hist_words(K) words.
+int64_t gsr_fused_chunks(int64_t K);
+hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_first, int64_t K,
+                                    uint32_t gx, int shift, int nbits, uint32_t *hist,
+                                    uint32_t *digit_total, uint32_t *keys_out, uint32_t *vals_out,
+                                    hipStream_t s);
 hipError_t gsr_launch_ranges(const uint32_t *tile_keys, int64_t K, uint32_t *ranges,
                              hipStream_t s);
 hipError_t gsr_launch_globalize_tiles(const uint32_t *local, int64_t K, uint32_t offset,

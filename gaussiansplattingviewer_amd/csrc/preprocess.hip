@@ -125,6 +125,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
     if (idx >= a.P) return;
     int32_t radius_out = 0;
     uint32_t strip_tiles = 0, all_tiles = 0;
+    uint2 strip_rect = make_uint2(0u, 0u);
     uint32_t key = 0xFFFFFFFFu;
 
     const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1],
@@ -174,6 +175,9 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
                 radius_out = r_int;
                 const uint32_t sy0 = max(rc.y0, a.row_begin), sy1 = min(rc.y1, a.row_end);
                 strip_tiles = sy1 > sy0 ? (rc.x1 - rc.x0) * (sy1 - sy0) : 0u;
+                if (strip_tiles)
+                    strip_rect = make_uint2(rc.x0 | ((rc.x1 - rc.x0) << 16),
+                                            (sy0 - a.row_begin) | ((sy1 - sy0) << 16));
                 if (strip_tiles) key = __float_as_uint(p_view.z);  // z > 0.2: bits are monotone
                 const float3 cd = cull_data(conic_a, conic_b, conic_c, opacity);
                 SplatRecord rec;
@@ -198,7 +202,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
         }
     }
     a.radii[idx] = radius_out;
-    a.strip_tiles[idx] = strip_tiles;
+    a.strip_rect[idx] = strip_rect;
     a.sort_keys[idx] = key;
     a.sort_vals[idx] = (uint32_t)idx;
     if (a.tiles_touched) a.tiles_touched[idx] = strip_tiles;

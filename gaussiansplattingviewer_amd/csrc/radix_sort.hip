@@ -28,34 +28,14 @@
 // concatenated in order, so each pass -- and the sort -- is stable.
 #include <algorithm>
 
-#include "gsr_internal.h"
+#include "radix_tile.h"
 
 using namespace gsr;
 
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kRadix = 256;
-
-// Exclusive scan over a block of kW waves (all threads call it; returns the prefix of v).
-template <int kW>
-__device__ __forceinline__ uint32_t blockw_exclusive_scan(uint32_t v, uint32_t *s_tmp,
-                                                          uint32_t &total) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t inc = wave_inclusive_scan(v);
-    if (lane == 63) s_tmp[w] = inc;
-    __syncthreads();
-    uint32_t pre = 0, tot = 0;
-#pragma unroll
-    for (int i = 0; i < kW; ++i) {
-        const uint32_t t = s_tmp[i];
-        pre += (i < w) ? t : 0u;
-        tot += t;
-    }
-    __syncthreads();
-    total = tot;
-    return pre + inc - v;
-}
+constexpr int kRadix = kRadixBins;
 
 // Reduce-then-scan, parameterised by waves per block (kW = 4: 4096-key tiles for the
 // P-sized depth sort; kW = 16: 16384-key tiles and 1024-thread blocks for the K-sized tile
@@ -126,20 +106,13 @@ __global__ __launch_bounds__(kW * 64) void k_rs_downsweep(
     uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out, int64_t n, int shift,
     int nbits, const uint32_t *__restrict__ hist, const uint32_t *__restrict__ digit_total,
     int64_t nb) {
-    constexpr int kThreads = kW * 64, kT = kThreads * kIt;
+    constexpr int kT = kW * 64 * kIt;
     __shared__ uint32_t s_keys[kT];
     __shared__ uint32_t s_vals[kT];
-    __shared__ uint32_t s_wcnt[kW][kRadix];
-    __shared__ uint32_t s_delta[kRadix];
-    __shared__ uint32_t s_tmp[2 * kW];
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const uint32_t mask = (1u << nbits) - 1u;
-    for (int i = tid; i < kW * kRadix; i += kThreads) (&s_wcnt[0][0])[i] = 0;
-    __syncthreads();
-
+    __shared__ RadixTileSmem<kW, kIt> sm;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t base = (int64_t)blockIdx.x * kT;
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint32_t k[kIt], v[kIt], rank[kIt];
+    uint32_t k[kIt], v[kIt];
 #pragma unroll
     for (int j = 0; j < kIt; ++j) {
         const int64_t e = base + w * (kT / kW) + j * 64 + lane;
@@ -147,63 +120,9 @@ __global__ __launch_bounds__(kW * 64) void k_rs_downsweep(
         k[j] = valid ? keys_in[e] : 0xFFFFFFFFu;  // tail -> largest digit, after every real key
         v[j] = valid ? vals_in[e] : 0u;
     }
-#pragma unroll
-    for (int j = 0; j < kIt; ++j) {
-        const uint32_t d = (k[j] >> shift) & mask;
-        uint64_t m = ~0ull;
-        for (int b = 0; b < nbits; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bal = __ballot(bit);
-            m &= bit ? bal : ~bal;
-        }
-        const uint32_t prior = s_wcnt[w][d];
-        rank[j] = prior + (uint32_t)__popcll(m & lt_mask);
-        if (lane == 63 - __clzll(m)) s_wcnt[w][d] = prior + (uint32_t)__popcll(m);
-    }
-    __syncthreads();
-
-    // Per digit (thread = digit): wave offsets, tile-local start, global destination.
-    {
-        const int d = tid;
-        uint32_t c[kW], sum = 0;
-        if (d < kRadix) {
-#pragma unroll
-            for (int i = 0; i < kW; ++i) {
-                c[i] = s_wcnt[i][d];
-                sum += c[i];
-            }
-        }
-        uint32_t tile_total, all_total;
-        const uint32_t local_start = blockw_exclusive_scan<kW>(d < kRadix ? sum : 0u, s_tmp, tile_total);
-        const uint32_t digit_start =
-            blockw_exclusive_scan<kW>(d < kRadix ? digit_total[d] : 0u, s_tmp + kW, all_total);
-        if (d < kRadix) {
-            s_delta[d] = digit_start + hist[(int64_t)d * nb + blockIdx.x] - local_start;
-            uint32_t run = local_start;
-#pragma unroll
-            for (int i = 0; i < kW; ++i) {
-                s_wcnt[i][d] = run;
-                run += c[i];
-            }
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kIt; ++j) {
-        const uint32_t d = (k[j] >> shift) & mask;
-        const uint32_t pos = s_wcnt[w][d] + rank[j];
-        s_keys[pos] = k[j];
-        s_vals[pos] = v[j];
-    }
-    __syncthreads();
     const int64_t rem = n - base;
-    const int valid = rem < kT ? (int)rem : kT;  // tail elements sit in the last slots
-    for (int i = tid; i < valid; i += kThreads) {
-        const uint32_t kk = s_keys[i];
-        const uint32_t g = s_delta[(kk >> shift) & mask] + (uint32_t)i;
-        keys_out[g] = kk;
-        vals_out[g] = s_vals[i];
-    }
+    radix_tile_scatter<kW, kIt>(k, v, rem < kT ? (int)rem : kT, shift, nbits, hist, nb,
+                                blockIdx.x, digit_total, keys_out, vals_out, sm, s_keys, s_vals);
 }
 
 // ---- onesweep -----------------------------------------------------------------------------
@@ -411,6 +330,12 @@ hipError_t gsr_onesweep_sort(uint32_t **keys, uint32_t **vals, uint32_t **keys_a
     return hipGetLastError();
 }
 
+hipError_t gsr_launch_digit_scan(uint32_t *hist, int64_t nb, uint32_t *digit_total,
+                                 hipStream_t s) {
+    hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, nb, digit_total);
+    return hipGetLastError();
+}
+
 int64_t gsr_radix_hist_words(int64_t n) {
     const int64_t nb = (n + 2047) / 2048;  // smallest tile shape (4 waves x 8 items)
     return (nb < 1 ? 1 : nb) * kRadix;
@@ -431,10 +356,11 @@ static void rts_pass(const uint32_t *k, const uint32_t *v, uint32_t *ko, uint32_
 
 hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
                                 uint32_t **vals_alt, int64_t n, int begin_bit, int end_bit,
-                                uint32_t *hist, uint32_t *digit_total, hipStream_t s, int shape) {
+                                uint32_t *hist, uint32_t *digit_total, hipStream_t s, int shape,
+                                int first_pass) {
     if (n <= 1) return hipSuccess;
     const GsrRadixPlan plan = gsr_radix_plan(begin_bit, end_bit);
-    for (int p = 0; p < plan.n; ++p) {
+    for (int p = first_pass; p < plan.n; ++p) {
         const int sh = plan.shift[p], nb = plan.nbits[p];
         switch (shape) {
             case 1: rts_pass<16, 16>(*keys, *vals, *keys_alt, *vals_alt, n, sh, nb, hist, digit_total, s); break;

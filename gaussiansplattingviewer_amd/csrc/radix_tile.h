@@ -1,0 +1,121 @@
+// radix_tile.h -- the downsweep step of the reduce-then-scan radix sort, as a device function:
+// rank one tile of (key, value) pairs stably by one digit and scatter it to its global
+// positions.  Shared by the radix sort (radix_sort.hip k_rs_downsweep) and by the fused
+// duplicate + first tile-sort pass (binning.hip k_dup_scatter), which generates its tile in
+// registers instead of loading it.
+#pragma once
+
+#include "gsr_internal.h"
+
+namespace gsr {
+
+constexpr int kRadixBins = 256;
+
+// Exclusive scan over a block of kW waves (all threads call it; returns the prefix of v).
+template <int kW>
+__device__ __forceinline__ uint32_t blockw_exclusive_scan(uint32_t v, uint32_t *s_tmp,
+                                                          uint32_t &total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t inc = wave_inclusive_scan(v);
+    if (lane == 63) s_tmp[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kW; ++i) {
+        const uint32_t t = s_tmp[i];
+        pre += (i < w) ? t : 0u;
+        tot += t;
+    }
+    __syncthreads();
+    total = tot;
+    return pre + inc - v;
+}
+
+template <int kW, int kIt>
+struct RadixTileSmem {
+    static constexpr int kT = kW * 64 * kIt;
+    uint32_t wcnt[kW][kRadixBins];
+    uint32_t delta[kRadixBins];
+    uint32_t tmp[2 * kW];
+};
+
+// Tile layout: wave w holds elements [w*kT/kW, (w+1)*kT/kW) of the tile, item j of lane l is
+// element w*kT/kW + j*64 + l.  Elements >= `valid` must carry key 0xFFFFFFFF (largest digit)
+// and are not written.  hist_tile = this tile's exclusive digit offset column entry
+// (hist[d * nb + tile]) as scanned by k_rs_scan; digit_total = per-digit totals.
+// s_keys / s_vals: kT words each (may alias storage the caller no longer needs: the first
+// write to them follows two block barriers).
+template <int kW, int kIt>
+__device__ __forceinline__ void radix_tile_scatter(
+    const uint32_t (&k)[kIt], const uint32_t (&v)[kIt], int valid, int shift, int nbits,
+    const uint32_t *__restrict__ hist, int64_t nb, uint32_t tile,
+    const uint32_t *__restrict__ digit_total, uint32_t *__restrict__ keys_out,
+    uint32_t *__restrict__ vals_out, RadixTileSmem<kW, kIt> &sm, uint32_t *s_keys,
+    uint32_t *s_vals) {
+    constexpr int kThreads = kW * 64;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t mask = (1u << nbits) - 1u;
+    for (int i = tid; i < kW * kRadixBins; i += kThreads) (&sm.wcnt[0][0])[i] = 0;
+    __syncthreads();
+
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t rank[kIt];
+#pragma unroll
+    for (int j = 0; j < kIt; ++j) {
+        const uint32_t d = (k[j] >> shift) & mask;
+        uint64_t m = ~0ull;
+        for (int b = 0; b < nbits; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bal = __ballot(bit);
+            m &= bit ? bal : ~bal;
+        }
+        const uint32_t prior = sm.wcnt[w][d];
+        rank[j] = prior + (uint32_t)__popcll(m & lt_mask);
+        if (lane == 63 - __clzll(m)) sm.wcnt[w][d] = prior + (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+
+    // Per digit (thread = digit): wave offsets, tile-local start, global destination.
+    {
+        const int d = tid;
+        uint32_t c[kW], sum = 0;
+        if (d < kRadixBins) {
+#pragma unroll
+            for (int i = 0; i < kW; ++i) {
+                c[i] = sm.wcnt[i][d];
+                sum += c[i];
+            }
+        }
+        uint32_t tile_total, all_total;
+        const uint32_t local_start =
+            blockw_exclusive_scan<kW>(d < kRadixBins ? sum : 0u, sm.tmp, tile_total);
+        const uint32_t digit_start = blockw_exclusive_scan<kW>(
+            d < kRadixBins ? digit_total[d] : 0u, sm.tmp + kW, all_total);
+        if (d < kRadixBins) {
+            sm.delta[d] = digit_start + hist[(int64_t)d * nb + tile] - local_start;
+            uint32_t run = local_start;
+#pragma unroll
+            for (int i = 0; i < kW; ++i) {
+                sm.wcnt[i][d] = run;
+                run += c[i];
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kIt; ++j) {
+        const uint32_t d = (k[j] >> shift) & mask;
+        const uint32_t pos = sm.wcnt[w][d] + rank[j];
+        s_keys[pos] = k[j];
+        s_vals[pos] = v[j];
+    }
+    __syncthreads();
+    for (int i = tid; i < valid; i += kThreads) {
+        const uint32_t kk = s_keys[i];
+        const uint32_t g = sm.delta[(kk >> shift) & mask] + (uint32_t)i;
+        keys_out[g] = kk;
+        vals_out[g] = s_vals[i];
+    }
+}
+
+}  // namespace gsr

@@ -40,6 +40,12 @@ CASES = {
     "C2_100k_1080p_sh0": (100_000, 1920, 1080, 0, 1, (0.0, 0.0, 4.0)),
     "oblique_30k_800x600_sh3": (30_000, 800, 600, 3, 4, (2.5, 1.0, -3.0)),
     "inside_cloud_20k_1160x522_sh3": (20_000, 1160, 522, 3, 5, (0.3, -0.2, 0.5)),
+    # image shapes that change the tile-sort plan: one tile (0 bits), one tile row, > 256
+    # tile columns, a narrow ragged image
+    "one_tile_5k_16x16_sh3": (5_000, 16, 16, 3, 6, (0.0, 0.0, 4.0)),
+    "one_row_8k_1000x12_sh3": (8_000, 1000, 12, 3, 7, (0.0, 0.0, 4.0)),
+    "wide_20k_4200x64_sh3": (20_000, 4200, 64, 3, 8, (0.0, 0.0, 4.0)),
+    "narrow_10k_33x700_sh3": (10_000, 33, 700, 3, 9, (0.0, 0.0, 4.0)),
 }
 
 
@@ -219,14 +225,24 @@ def test_headline_config_c3(gpu, c3_oracle, fast):
     assert_parity(hip, orc)
 
 
-def test_sort_implementations_agree(gpu):
-    """Reduce-then-scan (default) and onesweep radix sorts give identical binning."""
-    s = scene_inputs(synthetic_gaussians(300_000, 3, 21), static_camera(1920, 1080, (0.5, 0.2, 3.5)), 3)
-    rts = run_hip(s, gpu)
-    _set_option(gpu, _lib.GSR_OPT_SORT_ONESWEEP, 1)
+@pytest.mark.parametrize("variant", ["onesweep", "unfused", "shape0"])
+@pytest.mark.parametrize("size", [(1920, 1080), (16, 16), (4200, 64)])
+def test_sort_implementations_agree(gpu, variant, size):
+    """The default binning (duplicate fused with the first reduce-then-scan pass) and the
+    alternatives -- onesweep sort, separate duplicate kernel, another tile shape -- give
+    identical binning and images.  Sizes: 1 tile (tbits = 0) and > 8 bits of tile id in x."""
+    w, h = size
+    P = 300_000 if w * h > 10_000 else 20_000
+    s = scene_inputs(synthetic_gaussians(P, 3, 21), static_camera(w, h, (0.5, 0.2, 3.5)), 3)
+    ref = run_hip(s, gpu)
+    opt, val, default = {"onesweep": (_lib.GSR_OPT_SORT_ONESWEEP, 1, 0),
+                         "unfused": (_lib.GSR_OPT_FUSED_BINNING, 0, 1),
+                         "shape0": (_lib.GSR_OPT_TILE_SORT_SHAPE, 0, 3)}[variant]
+    _set_option(gpu, opt, val)
     try:
-        one = run_hip(s, gpu)
+        alt = run_hip(s, gpu)
     finally:
-        _set_option(gpu, _lib.GSR_OPT_SORT_ONESWEEP, 0)
+        _set_option(gpu, opt, default)
+    assert ref["num_rendered"] > 0
     for k in ("point_list", "point_tiles", "ranges", "color", "n_contrib"):
-        np.testing.assert_array_equal(one[k], rts[k], err_msg=k)
+        np.testing.assert_array_equal(alt[k], ref[k], err_msg=k)
