@@ -87,15 +87,51 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
     const int tx0 = (int)tx * GSR_TILE_X, ty0 = (int)ty * GSR_TILE_Y;
     const int px = tx0 + (w & 1) * 8 + (lane & 7), py = ty0 + (w >> 1) * 8 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
-    bool done = !inside;
     const float pfx = (float)px, pfy = (float)py;
 
     const uint2 range = a.ranges[ty_local * a.grid_x + tx];
-    float T = 1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
+    // A pixel is done (upstream's `done`) once T would fall below 1e-4; T then keeps its last
+    // value with the sign flipped, so one register carries both and the per-splat update needs
+    // no separate flag: a done pixel's test_T is <= 0, which no longer accumulates, and
+    // re-terminating it leaves -|T| unchanged.  |T| is upstream's final T.  A NaN T (NaN
+    // input) is never done, as upstream.
+    float T = inside ? 1.0f : -1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
     uint32_t last_contributor = 0;
 
+    auto composite = [&](const float4 g, const float4 q, const float blue, const uint32_t pos) {
+        const float dx = g.x - pfx, dy = g.y - pfy;
+        bool vis;
+        float alpha;
+        if (kFast) {
+            // log2(e) * power with the constants folded in: dx (a dx + b dy) + c dy^2
+            const float p2 = __builtin_fmaf(dx, __builtin_fmaf(g.z, dx, g.w * dy), q.x * dy * dy);
+            alpha = fminf(0.99f, q.y * __builtin_amdgcn_exp2f(p2));
+            vis = !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+        } else {
+            // upstream renderCUDA per-pixel body, same operation order
+            const float power = -0.5f * (g.z * dx * dx + q.x * dy * dy) - g.w * dx * dy;
+            alpha = fminf(0.99f, q.y * exp_core(power));
+            vis = !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+        }
+        const float test_T = T * (1 - alpha);
+        const bool acc = vis && !(test_T < 0.0001f);
+        const bool term = vis && (test_T < 0.0001f);
+        if (kFast) {
+            const float wgt = acc ? alpha * T : 0.0f;
+            C0 = __builtin_fmaf(q.z, wgt, C0);
+            C1 = __builtin_fmaf(q.w, wgt, C1);
+            C2 = __builtin_fmaf(blue, wgt, C2);
+        } else {
+            C0 = acc ? C0 + q.z * alpha * T : C0;
+            C1 = acc ? C1 + q.w * alpha * T : C1;
+            C2 = acc ? C2 + blue * alpha * T : C2;
+        }
+        T = acc ? test_T : (term ? -fabsf(T) : T);
+        last_contributor = acc ? pos : last_contributor;
+    };
+
     for (uint32_t start = range.x; start < range.y; start += kBatch) {
-        if (__syncthreads_count(done) == 256) break;
+        if (__syncthreads_count(T <= 0.0f) == 256) break;
         const uint32_t idx = start + tid;
         if (idx < range.y) {
             const SplatRecord r = a.records[a.point_list[idx]];
@@ -135,50 +171,28 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
         }
         // s_list[w] is written and read by this wave only: LDS ops of one wave execute in
         // order, so no barrier is needed before the reads below.
-        if (count == 0 || __ballot(!done) == 0ull) continue;
+        if (count == 0 || __ballot(!(T <= 0.0f)) == 0ull) continue;
 
-        int j = s_list[w][0];
-        float4 g = s_geo[j], q = s_opc[j];
-        float blue = s_blue[j];
-        for (int k = 0; k < count; ++k) {
-            const int jn = s_list[w][k + 1 < count ? k + 1 : k];
-            const float4 g_next = s_geo[jn], q_next = s_opc[jn];
-            const float blue_next = s_blue[jn];
-            const float dx = g.x - pfx, dy = g.y - pfy;
-            bool live;
-            float alpha;
-            if (kFast) {
-                // log2(e) * power with the constants folded in: dx (a dx + b dy) + c dy^2
-                const float p2 = __builtin_fmaf(dx, __builtin_fmaf(g.z, dx, g.w * dy), q.x * dy * dy);
-                alpha = fminf(0.99f, q.y * __builtin_amdgcn_exp2f(p2));
-                live = !done && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
-            } else {
-                // upstream renderCUDA per-pixel body, same operation order
-                const float power = -0.5f * (g.z * dx * dx + q.x * dy * dy) - g.w * dx * dy;
-                alpha = fminf(0.99f, q.y * exp_core(power));
-                live = !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-            }
-            const float test_T = T * (1 - alpha);
-            const bool term = live && (test_T < 0.0001f);
-            const bool acc = live && !(test_T < 0.0001f);
-            if (kFast) {
-                const float wgt = acc ? alpha * T : 0.0f;
-                C0 = __builtin_fmaf(q.z, wgt, C0);
-                C1 = __builtin_fmaf(q.w, wgt, C1);
-                C2 = __builtin_fmaf(blue, wgt, C2);
-            } else {
-                C0 = acc ? C0 + q.z * alpha * T : C0;
-                C1 = acc ? C1 + q.w * alpha * T : C1;
-                C2 = acc ? C2 + blue * alpha * T : C2;
-            }
-            T = acc ? test_T : T;
-            last_contributor = acc ? start - range.x + (uint32_t)j + 1u : last_contributor;
-            done = done || term;
-            j = jn;
-            g = g_next;
-            q = q_next;
-            blue = blue_next;
-            if ((k & 15) == 15 && __ballot(!done) == 0ull) break;
+        // Two splats per iteration; each one's LDS reads are issued as soon as its registers
+        // are free, a splat ahead of its use.
+        const uint32_t pos0 = start - range.x + 1u;  // upstream's `contributor` = list position
+        const int last = count - 1;
+        int j0 = s_list[w][0], j1 = s_list[w][min(1, last)];
+        float4 g0 = s_geo[j0], q0 = s_opc[j0], g1 = s_geo[j1], q1 = s_opc[j1];
+        float b0 = s_blue[j0], b1 = s_blue[j1];
+        for (int k = 0; k < count; k += 2) {
+            const int j2 = s_list[w][min(k + 2, last)], j3 = s_list[w][min(k + 3, last)];
+            composite(g0, q0, b0, pos0 + (uint32_t)j0);
+            g0 = s_geo[j2];
+            q0 = s_opc[j2];
+            b0 = s_blue[j2];
+            if (k + 1 < count) composite(g1, q1, b1, pos0 + (uint32_t)j1);
+            g1 = s_geo[j3];
+            q1 = s_opc[j3];
+            b1 = s_blue[j3];
+            j0 = j2;
+            j1 = j3;
+            if ((k & 30) == 30 && __ballot(!(T <= 0.0f)) == 0ull) break;
         }
     }
 
@@ -186,11 +200,12 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
         const int row = py - a.y0;
         const size_t pid = (size_t)row * a.W + px;
         const size_t plane = (size_t)a.rows_out * a.W;
-        if (a.final_T) a.final_T[pid] = T;
+        const float Tf = fabsf(T);
+        if (a.final_T) a.final_T[pid] = Tf;
         if (a.n_contrib) a.n_contrib[pid] = last_contributor;
-        a.out_color[pid] = C0 + T * a.bg[0];
-        a.out_color[plane + pid] = C1 + T * a.bg[1];
-        a.out_color[2 * plane + pid] = C2 + T * a.bg[2];
+        a.out_color[pid] = C0 + Tf * a.bg[0];
+        a.out_color[plane + pid] = C1 + Tf * a.bg[1];
+        a.out_color[2 * plane + pid] = C2 + Tf * a.bg[2];
     }
 }
 
