@@ -74,13 +74,19 @@ constexpr int kBatch = 256;  // splats staged in LDS per round
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 
+// One staged splat as the inner loop reads it: three 16-B LDS reads from one address.
+struct StagedSplat {
+    float4 g;  // x, y, conic a, conic b      (fast: prescaled a, b)
+    float4 q;  // conic c, opacity, r, g      (fast: prescaled c)
+    float4 e;  // b, list position + 1 (uint bits: upstream's `contributor`), -, -
+};
+
 template <bool kFast>
 __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
-    __shared__ float4 s_geo[kBatch];   // x, y, conic.a, conic.b   (fast: prescaled a, b)
-    __shared__ float4 s_opc[kBatch];   // conic.c, opacity, r, g    (fast: prescaled c)
-    __shared__ float s_blue[kBatch];   // b
-    __shared__ uint8_t s_mask[kBatch]; // quadrant bits of each staged splat
-    __shared__ uint8_t s_list[4][kBatch];
+    // slot kBatch: an opacity-0 splat that pads odd lists (alpha 0 < 1/255: never visible)
+    __shared__ StagedSplat s_spl[kBatch + 1];
+    __shared__ uint8_t s_mask[kBatch];          // quadrant bits of each staged splat
+    __shared__ uint16_t s_list[4][kBatch + 1];  // per wave: byte offsets into s_spl
 
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t tx = blockIdx.x, ty_local = blockIdx.y, ty = a.row_begin + ty_local;
@@ -88,6 +94,11 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
     const int px = tx0 + (w & 1) * 8 + (lane & 7), py = ty0 + (w >> 1) * 8 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
     const float pfx = (float)px, pfy = (float)py;
+    if (tid == 0) {
+        s_spl[kBatch].g = make_float4(0.f, 0.f, 0.f, 0.f);
+        s_spl[kBatch].q = make_float4(0.f, 0.f, 0.f, 0.f);
+        s_spl[kBatch].e = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 
     const uint2 range = a.ranges[ty_local * a.grid_x + tx];
     // A pixel is done (upstream's `done`) once T would fall below 1e-4; T then keeps its last
@@ -98,37 +109,42 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
     float T = inside ? 1.0f : -1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
     uint32_t last_contributor = 0;
 
-    auto composite = [&](const float4 g, const float4 q, const float blue, const uint32_t pos) {
-        const float dx = g.x - pfx, dy = g.y - pfy;
-        bool vis;
-        float alpha;
+    auto composite = [&](const StagedSplat &sp) {
+        const float dx = sp.g.x - pfx, dy = sp.g.y - pfy;
+        bool vis, acc, term;
+        float test_T, wgt;
         if (kFast) {
             // log2(e) * power with the constants folded in: dx (a dx + b dy) + c dy^2
-            const float p2 = __builtin_fmaf(dx, __builtin_fmaf(g.z, dx, g.w * dy), q.x * dy * dy);
-            alpha = fminf(0.99f, q.y * __builtin_amdgcn_exp2f(p2));
+            const float p2 =
+                __builtin_fmaf(dx, __builtin_fmaf(sp.g.z, dx, sp.g.w * dy), sp.q.x * dy * dy);
+            const float alpha = fminf(0.99f, sp.q.y * __builtin_amdgcn_exp2f(p2));
             vis = !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+            const float aT = alpha * T;
+            test_T = T - aT;  // T (1 - alpha), rounded differently
+            acc = vis && !(test_T < 0.0001f);
+            term = vis && (test_T < 0.0001f);
+            wgt = acc ? aT : 0.0f;
+            C0 = __builtin_fmaf(sp.q.z, wgt, C0);
+            C1 = __builtin_fmaf(sp.q.w, wgt, C1);
+            C2 = __builtin_fmaf(sp.e.x, wgt, C2);
         } else {
             // upstream renderCUDA per-pixel body, same operation order
-            const float power = -0.5f * (g.z * dx * dx + q.x * dy * dy) - g.w * dx * dy;
-            alpha = fminf(0.99f, q.y * exp_core(power));
+            const float power =
+                -0.5f * (sp.g.z * dx * dx + sp.q.x * dy * dy) - sp.g.w * dx * dy;
+            const float alpha = fminf(0.99f, sp.q.y * exp_core(power));
             vis = !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-        }
-        const float test_T = T * (1 - alpha);
-        const bool acc = vis && !(test_T < 0.0001f);
-        const bool term = vis && (test_T < 0.0001f);
-        if (kFast) {
-            const float wgt = acc ? alpha * T : 0.0f;
-            C0 = __builtin_fmaf(q.z, wgt, C0);
-            C1 = __builtin_fmaf(q.w, wgt, C1);
-            C2 = __builtin_fmaf(blue, wgt, C2);
-        } else {
-            C0 = acc ? C0 + q.z * alpha * T : C0;
-            C1 = acc ? C1 + q.w * alpha * T : C1;
-            C2 = acc ? C2 + blue * alpha * T : C2;
+            test_T = T * (1 - alpha);
+            acc = vis && !(test_T < 0.0001f);
+            term = vis && (test_T < 0.0001f);
+            C0 = acc ? C0 + sp.q.z * alpha * T : C0;
+            C1 = acc ? C1 + sp.q.w * alpha * T : C1;
+            C2 = acc ? C2 + sp.e.x * alpha * T : C2;
         }
         T = acc ? test_T : (term ? -fabsf(T) : T);
-        last_contributor = acc ? pos : last_contributor;
+        last_contributor = acc ? __float_as_uint(sp.e.y) : last_contributor;
     };
+    const char *lds = reinterpret_cast<const char *>(s_spl);
+    auto fetch = [&](uint32_t off) { return *reinterpret_cast<const StagedSplat *>(lds + off); };
 
     for (uint32_t start = range.x; start < range.y; start += kBatch) {
         if (__syncthreads_count(T <= 0.0f) == 256) break;
@@ -145,54 +161,62 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
                     ((uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0, X0 + 7, Y0 + 8, Y0 + 15) << 2) |
                     ((uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0 + 8, X0 + 15, Y0 + 8, Y0 + 15) << 3);
             }
+            StagedSplat st;
             if (kFast) {
                 const float kL2e = 1.4426950408889634f;
-                s_geo[tid] = make_float4(r.a.x, r.a.y, r.a.z * (-0.5f * kL2e), r.a.w * (-kL2e));
-                s_opc[tid] = make_float4(r.b.x * (-0.5f * kL2e), r.b.y, r.b.z, r.b.w);
+                st.g = make_float4(r.a.x, r.a.y, r.a.z * (-0.5f * kL2e), r.a.w * (-kL2e));
+                st.q = make_float4(r.b.x * (-0.5f * kL2e), r.b.y, r.b.z, r.b.w);
             } else {
-                s_geo[tid] = r.a;
-                s_opc[tid] = r.b;
+                st.g = r.a;
+                st.q = r.b;
             }
-            s_blue[tid] = r.c.x;
+            st.e = make_float4(r.c.x, __uint_as_float(idx - range.x + 1u), 0.0f, 0.0f);
+            s_spl[tid] = st;
             s_mask[tid] = (uint8_t)m;
         }
         __syncthreads();
         const int n = (int)min((uint32_t)kBatch, range.y - start);
 
-        // This wave's splats of the batch, in list order.
+        // This wave's splats of the batch, in list order, padded to an even count.
         int count = 0;
         for (int base = 0; base < n; base += 64) {
             const int j = base + lane;
             const bool keep = j < n && ((s_mask[j] >> w) & 1u);
             const uint64_t bal = __ballot(keep);
             const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-            if (keep) s_list[w][count + __popcll(bal & lt)] = (uint8_t)j;
+            if (keep)
+                s_list[w][count + __popcll(bal & lt)] = (uint16_t)(j * sizeof(StagedSplat));
             count += __popcll(bal);
+        }
+        if (count & 1) {
+            if (lane == 0) s_list[w][count] = (uint16_t)(kBatch * sizeof(StagedSplat));
+            ++count;
         }
         // s_list[w] is written and read by this wave only: LDS ops of one wave execute in
         // order, so no barrier is needed before the reads below.
         if (count == 0 || __ballot(!(T <= 0.0f)) == 0ull) continue;
 
-        // Two splats per iteration; each one's LDS reads are issued as soon as its registers
-        // are free, a splat ahead of its use.
-        const uint32_t pos0 = start - range.x + 1u;  // upstream's `contributor` = list position
-        const int last = count - 1;
-        int j0 = s_list[w][0], j1 = s_list[w][min(1, last)];
-        float4 g0 = s_geo[j0], q0 = s_opc[j0], g1 = s_geo[j1], q1 = s_opc[j1];
-        float b0 = s_blue[j0], b1 = s_blue[j1];
-        for (int k = 0; k < count; k += 2) {
-            const int j2 = s_list[w][min(k + 2, last)], j3 = s_list[w][min(k + 3, last)];
-            composite(g0, q0, b0, pos0 + (uint32_t)j0);
-            g0 = s_geo[j2];
-            q0 = s_opc[j2];
-            b0 = s_blue[j2];
-            if (k + 1 < count) composite(g1, q1, b1, pos0 + (uint32_t)j1);
-            g1 = s_geo[j3];
-            q1 = s_opc[j3];
-            b1 = s_blue[j3];
-            j0 = j2;
-            j1 = j3;
-            if ((k & 30) == 30 && __ballot(!(T <= 0.0f)) == 0ull) break;
+        // Two splats per iteration, straight-line (the scheduler interleaves their
+        // T-independent parts); the next pair's LDS reads are issued before this pair runs.
+        // A/B register sets alternate so no prefetched splat is ever copied.
+        const uint16_t *list = s_list[w];
+        auto next2 = [&](int k) { return k + 2 < count ? k + 2 : count - 2; };
+        StagedSplat a0 = fetch(list[0]), a1 = fetch(list[1]);
+        for (int k = 0;;) {
+            int kn = next2(k);
+            const StagedSplat b0 = fetch(list[kn]), b1 = fetch(list[kn + 1]);
+            composite(a0);
+            composite(a1);
+            k += 2;
+            if (k >= count) break;
+            kn = next2(k);
+            a0 = fetch(list[kn]);
+            a1 = fetch(list[kn + 1]);
+            composite(b0);
+            composite(b1);
+            k += 2;
+            if (k >= count) break;
+            if ((k & 28) == 0 && __ballot(!(T <= 0.0f)) == 0ull) break;
         }
     }
 
@@ -227,17 +251,49 @@ __global__ __launch_bounds__(128) void k_blend_fast2(const GsrBlendArgs a) {
     const int tx0 = (int)tx * GSR_TILE_X, ty0 = (int)ty * GSR_TILE_Y;
     const int pxa = tx0 + (lane & 7), pxb = pxa + 8, py = ty0 + w * 8 + (lane >> 3);
     const bool in_a = pxa < a.W && py < a.H, in_b = pxb < a.W && py < a.H;
-    bool done_a = !in_a, done_b = !in_b;
     const v2f pfx = {(float)pxa, (float)pxb};
     const float pfy = (float)py;
 
     const uint2 range = a.ranges[ty_local * a.grid_x + tx];
-    v2f T = {1.0f, 1.0f}, C0 = {0.0f, 0.0f}, C1 = {0.0f, 0.0f}, C2 = {0.0f, 0.0f};
+    // done carried in the sign of T, as in k_blend
+    v2f T = {in_a ? 1.0f : -1.0f, in_b ? 1.0f : -1.0f};
+    v2f C0 = {0.0f, 0.0f}, C1 = {0.0f, 0.0f}, C2 = {0.0f, 0.0f};
     uint32_t last_a = 0, last_b = 0;
     const float kL2e = 1.4426950408889634f;
+    auto live_any = [&]() { return !(T.x <= 0.0f) || !(T.y <= 0.0f); };
+
+    auto composite = [&](const float4 g, const float4 q, const float blue, const uint32_t pos) {
+        const v2f dx = (v2f)g.x - pfx;
+        const float dy = g.y - pfy;
+        const v2f ady = __builtin_elementwise_fma((v2f)g.z, dx, (v2f)(g.w * dy));
+        const v2f p2 = __builtin_elementwise_fma(dx, ady, (v2f)(q.x * dy * dy));
+        v2f e;
+        e.x = __builtin_amdgcn_exp2f(p2.x);
+        e.y = __builtin_amdgcn_exp2f(p2.y);
+        const v2f oe = (v2f)q.y * e;
+        v2f alpha;
+        alpha.x = fminf(0.99f, oe.x);
+        alpha.y = fminf(0.99f, oe.y);
+        const v2f test_T = T * ((v2f)1.0f - alpha);
+        const v2f aT = alpha * T;
+        const bool vis_a = !(p2.x > 0.0f) && !(alpha.x < 1.0f / 255.0f);
+        const bool vis_b = !(p2.y > 0.0f) && !(alpha.y < 1.0f / 255.0f);
+        const bool lo_a = test_T.x < 0.0001f, lo_b = test_T.y < 0.0001f;
+        const bool acc_a = vis_a && !lo_a, acc_b = vis_b && !lo_b;
+        v2f wgt;
+        wgt.x = acc_a ? aT.x : 0.0f;
+        wgt.y = acc_b ? aT.y : 0.0f;
+        C0 = __builtin_elementwise_fma((v2f)q.z, wgt, C0);
+        C1 = __builtin_elementwise_fma((v2f)q.w, wgt, C1);
+        C2 = __builtin_elementwise_fma((v2f)blue, wgt, C2);
+        T.x = acc_a ? test_T.x : ((vis_a && lo_a) ? -fabsf(T.x) : T.x);
+        T.y = acc_b ? test_T.y : ((vis_b && lo_b) ? -fabsf(T.y) : T.y);
+        last_a = acc_a ? pos : last_a;
+        last_b = acc_b ? pos : last_b;
+    };
 
     for (uint32_t start = range.x; start < range.y; start += kBatch) {
-        if (__syncthreads_count(done_a && done_b) == 128) break;
+        if (__syncthreads_count(!live_any()) == 128) break;
         for (int t = tid; t < kBatch; t += 128) {
             const uint32_t idx = start + t;
             if (idx >= range.y) break;
@@ -269,70 +325,47 @@ __global__ __launch_bounds__(128) void k_blend_fast2(const GsrBlendArgs a) {
             if (keep) s_list[w][count + __popcll(bal & lt)] = (uint8_t)j;
             count += __popcll(bal);
         }
-        if (count == 0 || __ballot(!(done_a && done_b)) == 0ull) continue;
+        if (count == 0 || __ballot(live_any()) == 0ull) continue;
 
-        int j = s_list[w][0];
-        float4 g = s_geo[j], q = s_opc[j];
-        float blue = s_blue[j];
-        for (int k = 0; k < count; ++k) {
-            const int jn = s_list[w][k + 1 < count ? k + 1 : k];
-            const float4 g_next = s_geo[jn], q_next = s_opc[jn];
-            const float blue_next = s_blue[jn];
-            const v2f dx = (v2f)g.x - pfx;
-            const float dy = g.y - pfy;
-            const v2f ady = __builtin_elementwise_fma((v2f)g.z, dx, (v2f)(g.w * dy));
-            const v2f p2 = __builtin_elementwise_fma(dx, ady, (v2f)(q.x * dy * dy));
-            v2f e;
-            e.x = __builtin_amdgcn_exp2f(p2.x);
-            e.y = __builtin_amdgcn_exp2f(p2.y);
-            const v2f oe = (v2f)q.y * e;
-            v2f alpha;
-            alpha.x = fminf(0.99f, oe.x);
-            alpha.y = fminf(0.99f, oe.y);
-            const v2f test_T = T * ((v2f)1.0f - alpha);
-            const bool live_a = !done_a && !(p2.x > 0.0f) && !(alpha.x < 1.0f / 255.0f);
-            const bool live_b = !done_b && !(p2.y > 0.0f) && !(alpha.y < 1.0f / 255.0f);
-            const bool acc_a = live_a && !(test_T.x < 0.0001f);
-            const bool acc_b = live_b && !(test_T.y < 0.0001f);
-            const v2f aT = alpha * T;
-            v2f wgt;
-            wgt.x = acc_a ? aT.x : 0.0f;
-            wgt.y = acc_b ? aT.y : 0.0f;
-            C0 = __builtin_elementwise_fma((v2f)q.z, wgt, C0);
-            C1 = __builtin_elementwise_fma((v2f)q.w, wgt, C1);
-            C2 = __builtin_elementwise_fma((v2f)blue, wgt, C2);
-            T.x = acc_a ? test_T.x : T.x;
-            T.y = acc_b ? test_T.y : T.y;
-            const uint32_t pos = start - range.x + (uint32_t)j + 1u;
-            last_a = acc_a ? pos : last_a;
-            last_b = acc_b ? pos : last_b;
-            done_a = done_a || (live_a && (test_T.x < 0.0001f));
-            done_b = done_b || (live_b && (test_T.y < 0.0001f));
-            j = jn;
-            g = g_next;
-            q = q_next;
-            blue = blue_next;
-            if ((k & 15) == 15 && __ballot(!(done_a && done_b)) == 0ull) break;
+        const uint32_t pos0 = start - range.x + 1u;
+        const int last = count - 1;
+        int j0 = s_list[w][0], j1 = s_list[w][min(1, last)];
+        float4 g0 = s_geo[j0], q0 = s_opc[j0], g1 = s_geo[j1], q1 = s_opc[j1];
+        float b0 = s_blue[j0], b1 = s_blue[j1];
+        for (int k = 0; k < count; k += 2) {
+            const int j2 = s_list[w][min(k + 2, last)], j3 = s_list[w][min(k + 3, last)];
+            composite(g0, q0, b0, pos0 + (uint32_t)j0);
+            g0 = s_geo[j2];
+            q0 = s_opc[j2];
+            b0 = s_blue[j2];
+            if (k + 1 < count) composite(g1, q1, b1, pos0 + (uint32_t)j1);
+            g1 = s_geo[j3];
+            q1 = s_opc[j3];
+            b1 = s_blue[j3];
+            j0 = j2;
+            j1 = j3;
+            if ((k & 30) == 30 && __ballot(live_any()) == 0ull) break;
         }
     }
 
     const int row = py - a.y0;
     const size_t plane = (size_t)a.rows_out * a.W;
+    const float Ta = fabsf(T.x), Tb = fabsf(T.y);
     if (in_a) {
         const size_t pid = (size_t)row * a.W + pxa;
-        if (a.final_T) a.final_T[pid] = T.x;
+        if (a.final_T) a.final_T[pid] = Ta;
         if (a.n_contrib) a.n_contrib[pid] = last_a;
-        a.out_color[pid] = C0.x + T.x * a.bg[0];
-        a.out_color[plane + pid] = C1.x + T.x * a.bg[1];
-        a.out_color[2 * plane + pid] = C2.x + T.x * a.bg[2];
+        a.out_color[pid] = C0.x + Ta * a.bg[0];
+        a.out_color[plane + pid] = C1.x + Ta * a.bg[1];
+        a.out_color[2 * plane + pid] = C2.x + Ta * a.bg[2];
     }
     if (in_b) {
         const size_t pid = (size_t)row * a.W + pxb;
-        if (a.final_T) a.final_T[pid] = T.y;
+        if (a.final_T) a.final_T[pid] = Tb;
         if (a.n_contrib) a.n_contrib[pid] = last_b;
-        a.out_color[pid] = C0.y + T.y * a.bg[0];
-        a.out_color[plane + pid] = C1.y + T.y * a.bg[1];
-        a.out_color[2 * plane + pid] = C2.y + T.y * a.bg[2];
+        a.out_color[pid] = C0.y + Tb * a.bg[0];
+        a.out_color[plane + pid] = C1.y + Tb * a.bg[1];
+        a.out_color[2 * plane + pid] = C2.y + Tb * a.bg[2];
     }
 }
 
