@@ -55,8 +55,12 @@ def parse():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sort-shape", type=int, default=None, help="GSR_OPT_TILE_SORT_SHAPE (tuning)")
+    ap.add_argument("--depth-sort-shape", type=int, default=None,
+                    help="GSR_OPT_DEPTH_SORT_SHAPE (tuning)")
     ap.add_argument("--onesweep", action="store_true", help="GSR_OPT_SORT_ONESWEEP (tuning)")
     ap.add_argument("--unfused", action="store_true", help="GSR_OPT_FUSED_BINNING=0 (tuning)")
+    ap.add_argument("--blend-blocks", action="store_true",
+                    help="GSR_OPT_BLEND_WAVE_QUADRANTS=0: 4-wave block per tile (tuning)")
     ap.add_argument("--blend", default="fast", choices=["exact", "fast", "packed"],
                     help="blend arithmetic: GSR_OPT_BLEND_FAST (default) or upstream's exact "
                          "operation order")
@@ -157,8 +161,13 @@ def main():
     _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_BLEND_FAST,
                                   {"exact": 0, "fast": 1, "packed": 2}[args.blend]),
                "gsr_set_option")
+    if args.depth_sort_shape is not None:
+        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_DEPTH_SORT_SHAPE, args.depth_sort_shape),
+                   "opt")
     if args.sort_shape is not None:
         _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_TILE_SORT_SHAPE, args.sort_shape), "opt")
+    if args.blend_blocks:
+        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_BLEND_WAVE_QUADRANTS, 0), "opt")
     if args.unfused:
         _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_FUSED_BINNING, 0), "opt")
     if args.onesweep:

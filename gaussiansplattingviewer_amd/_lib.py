@@ -5,6 +5,7 @@ the library is missing or has no HIP device, every entry point raises RuntimeErr
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import threading
@@ -18,6 +19,8 @@ GSR_OPT_BLEND_FAST = 2
 GSR_OPT_SORT_ONESWEEP = 3
 GSR_OPT_TILE_SORT_SHAPE = 4
 GSR_OPT_FUSED_BINNING = 5
+GSR_OPT_BLEND_WAVE_QUADRANTS = 6
+GSR_OPT_DEPTH_SORT_SHAPE = 7
 
 # Symbols include/gsr.h declares (checked by the CPU test suite).
 EXPORTED_SYMBOLS = (
@@ -133,6 +136,21 @@ def context(device_index: int) -> ctypes.c_void_p:
             check(lib.gsr_create(ctypes.byref(ctx)), "gsr_create")
         _contexts[device_index] = ctx
         return ctx
+
+
+def release_contexts() -> None:
+    """Destroy every gsr_context (registered with atexit; a diagnostics build reports its
+    counters from gsr_destroy)."""
+    with _lock:
+        lib = _lib
+        if lib is None or not _contexts:
+            return
+        for ctx in _contexts.values():
+            lib.gsr_destroy(ctx)
+        _contexts.clear()
+
+
+atexit.register(release_contexts)
 
 
 def stage_names() -> list[str]:

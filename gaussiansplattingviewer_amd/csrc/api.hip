@@ -5,6 +5,7 @@
 // (rasterizer_impl.cu), which the viewer reaches through renderer_cuda.py:211-224.
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -62,11 +63,14 @@ struct gsr_context {
     int fast = 1;
     int onesweep = 0;
     int tile_sort_shape = 3;  // 8 waves x 8 keys/lane: fastest measured
+    int depth_sort_shape = 3;  // 8x8: 78 us vs 89 for 4x16 at 1M keys (bench, round 1)
     int fused_binning = 1;    // duplicate fused with the first tile-sort pass
+    int blend_wave_quadrants = 1;
     // Stage timing: a ring of event sets, one per forward, read back after the timed region.
     bool timing = false;
     int64_t timed_frames = 0;
     hipEvent_t ev[kTimingRing][kStages + 1] = {};
+    unsigned long long *blend_stamps = nullptr;  // diagnostics, env GSR_DEBUG_BLEND_STAMPS
 };
 
 namespace {
@@ -193,6 +197,13 @@ int gsr_create(gsr_context **out) {
                 return fail(GSR_E_HIP, "gsr_create: hipEventCreate failed");
             }
         }
+    if (std::getenv("GSR_DEBUG_BLEND_STAMPS")) {
+        if (hipMalloc(reinterpret_cast<void **>(&ctx->blend_stamps), 256 * 8 * 8) != hipSuccess ||
+            hipMemset(ctx->blend_stamps, 0, 256 * 8 * 8) != hipSuccess) {
+            (void)hipGetLastError();
+            ctx->blend_stamps = nullptr;
+        }
+    }
     *out = ctx;
     return GSR_OK;
 }
@@ -213,6 +224,18 @@ void gsr_destroy(gsr_context *ctx) {
         for (auto &e : set)
             if (e) (void)hipEventDestroy(e);
     if (ctx->h_total) (void)hipHostFree(ctx->h_total);
+    if (ctx->blend_stamps) {
+        static unsigned long long sh[256 * 8];
+        unsigned long long h[8] = {};
+        (void)hipMemcpy(sh, ctx->blend_stamps, sizeof(sh), hipMemcpyDeviceToHost);
+        for (int i = 0; i < 256 * 8; ++i) h[i % 8] += sh[i];
+        const double waves = h[5] ? (double)h[5] : 1.0;
+        std::fprintf(stderr,
+                     "[gsr blend stamps] per wave: staging+barriers %.0f, lists %.0f, "
+                     "compositing %.0f cycles; %.2f batches, %.1f splats composited\n",
+                     h[0] / waves, h[1] / waves, h[2] / waves, h[3] / waves, h[4] / waves);
+        (void)hipFree(ctx->blend_stamps);
+    }
     delete ctx;
 }
 
@@ -239,12 +262,21 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
         ctx->onesweep = value ? 1 : 0;
         return GSR_OK;
     }
+    if (option == GSR_OPT_BLEND_WAVE_QUADRANTS) {
+        ctx->blend_wave_quadrants = value ? 1 : 0;
+        return GSR_OK;
+    }
     if (option == GSR_OPT_FUSED_BINNING) {
         ctx->fused_binning = value ? 1 : 0;
         return GSR_OK;
     }
+    if (option == GSR_OPT_DEPTH_SORT_SHAPE) {
+        if (value < 0 || value > 5) return fail(GSR_E_INVALID, "gsr_set_option: shape 0..5");
+        ctx->depth_sort_shape = (int)value;
+        return GSR_OK;
+    }
     if (option == GSR_OPT_TILE_SORT_SHAPE) {
-        if (value < 0 || value > 4) return fail(GSR_E_INVALID, "gsr_set_option: shape 0..4");
+        if (value < 0 || value > 5) return fail(GSR_E_INVALID, "gsr_set_option: shape 0..5");
         ctx->tile_sort_shape = (int)value;
         return GSR_OK;
     }
@@ -416,7 +448,8 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
                                   onesweep_ws(ctx, 0), s),
                 "depth sort launch");
     } else {
-        GSR_HIP(gsr_radix_sort_pairs(&dk, &dv, &dk_alt, &dv_alt, P, 0, 32, hist, digit_total, s),
+        GSR_HIP(gsr_radix_sort_pairs(&dk, &dv, &dk_alt, &dv_alt, P, 0, 32, hist, digit_total, s,
+                                     ctx->depth_sort_shape),
                 "depth sort launch");
     }
     GSR_TRY(stage_end(1));
@@ -508,6 +541,8 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     ba.n_contrib = out->n_contrib;
     ba.cull = ctx->cull;
     ba.fast = ctx->fast;
+    ba.wave_quadrants = ctx->blend_wave_quadrants;
+    ba.stamps = ctx->blend_stamps;
     GSR_HIP(gsr_launch_blend(ba, s), "blend launch");
     GSR_TRY(stage_end(6));
 
@@ -584,7 +619,8 @@ int gsr_depth_argsort(gsr_context *ctx, const float *xyz, int64_t P, const float
     } else {
         GSR_HIP(gsr_radix_sort_pairs(&k, &v, &ka, &va, P, 0, 32,
                                      static_cast<uint32_t *>(ctx->hist.p),
-                                     static_cast<uint32_t *>(ctx->digit_total.p), s),
+                                     static_cast<uint32_t *>(ctx->digit_total.p), s,
+                                     ctx->depth_sort_shape),
                 "depth argsort launch");
     }
     GSR_HIP(gsr_launch_index_to_i32(v, P, out_index, s), "index launch");

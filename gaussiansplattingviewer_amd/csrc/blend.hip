@@ -81,7 +81,10 @@ struct StagedSplat {
     float4 e;  // b, list position + 1 (uint bits: upstream's `contributor`), -, -
 };
 
-template <bool kFast>
+// Diagnostics build (kStamp): lane 0 of every wave sums s_memtime cycles per phase into
+// a.stamps[shard * 8 + 0..5] = {staging incl. barriers, list compaction, compositing, batches, splats
+// composited, waves}.
+template <bool kFast, bool kStamp = false>
 __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
     // slot kBatch: an opacity-0 splat that pads odd lists (alpha 0 < 1/255: never visible)
     __shared__ StagedSplat s_spl[kBatch + 1];
@@ -146,6 +149,8 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
     const char *lds = reinterpret_cast<const char *>(s_spl);
     auto fetch = [&](uint32_t off) { return *reinterpret_cast<const StagedSplat *>(lds + off); };
 
+    unsigned long long t_stage = 0, t_list = 0, t_comp = 0, n_batch = 0, n_splat = 0, t0 = 0;
+    if (kStamp) t0 = __builtin_amdgcn_s_memtime();
     for (uint32_t start = range.x; start < range.y; start += kBatch) {
         if (__syncthreads_count(T <= 0.0f) == 256) break;
         const uint32_t idx = start + tid;
@@ -175,6 +180,12 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
             s_mask[tid] = (uint8_t)m;
         }
         __syncthreads();
+        if (kStamp) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            t_stage += t1 - t0;
+            t0 = t1;
+            ++n_batch;
+        }
         const int n = (int)min((uint32_t)kBatch, range.y - start);
 
         // This wave's splats of the batch, in list order, padded to an even count.
@@ -218,6 +229,171 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
             if (k >= count) break;
             if ((k & 28) == 0 && __ballot(!(T <= 0.0f)) == 0ull) break;
         }
+        if (kStamp) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            t_comp += t1 - t0;
+            t0 = t1;
+            n_splat += (unsigned long long)count;
+        }
+    }
+    if (kStamp && lane == 0) {  // 256 shards of 8 counters: same-address atomics serialise
+        unsigned long long *st = a.stamps + 8 * ((blockIdx.x + blockIdx.y * 17 + w) & 255);
+        atomicAdd(&st[0], t_stage);
+        atomicAdd(&st[1], t_list);
+        atomicAdd(&st[2], t_comp);
+        atomicAdd(&st[3], n_batch);
+        atomicAdd(&st[4], n_splat);
+        atomicAdd(&st[5], 1ull);
+    }
+
+    if (inside) {
+        const int row = py - a.y0;
+        const size_t pid = (size_t)row * a.W + px;
+        const size_t plane = (size_t)a.rows_out * a.W;
+        const float Tf = fabsf(T);
+        if (a.final_T) a.final_T[pid] = Tf;
+        if (a.n_contrib) a.n_contrib[pid] = last_contributor;
+        a.out_color[pid] = C0 + Tf * a.bg[0];
+        a.out_color[plane + pid] = C1 + Tf * a.bg[1];
+        a.out_color[2 * plane + pid] = C2 + Tf * a.bg[2];
+    }
+}
+
+// One wave per (tile, 8x8 quadrant), 64-thread blocks, no block barriers: each wave streams
+// its tile's list 64 splats at a time, culls them against its own quadrant, compacts the
+// survivors and composites them, and stops as soon as its own 64 pixels are done -- so a
+// quadrant never waits for the slowest quadrant of its tile (the 4-wave kernel's batch
+// barriers cost ~40 % of wave time, measured with GSR_DEBUG_BLEND_STAMPS).  Record gathers
+// are software-pipelined: a chunk's records are loaded while the previous chunk is
+// composited, their ids one chunk earlier still.  Blocks are mapped XCD-aware: hardware
+// dispatches block b to XCD b % 8, so work item (b % 8) * per_xcd + b / 8 keeps the four
+// quadrants of a tile (and neighbouring tiles) on one XCD's L2.
+template <bool kFast>
+__global__ __launch_bounds__(64) void k_blend_q(const GsrBlendArgs a, uint32_t n_work,
+                                                uint32_t per_xcd) {
+    __shared__ StagedSplat s_spl[64 + 1];  // slot 64: opacity-0 pad
+    __shared__ uint16_t s_list[64 + 2];
+
+    const uint32_t b = blockIdx.x;
+    const uint32_t work = (b & 7u) * per_xcd + (b >> 3);
+    if (work >= n_work) return;
+    const int lane = threadIdx.x;
+    const uint32_t tile = work >> 2, quad = work & 3u;
+    const uint32_t tx = tile % a.grid_x, ty_local = tile / a.grid_x, ty = a.row_begin + ty_local;
+    const int qx0 = (int)tx * GSR_TILE_X + (int)(quad & 1u) * 8;
+    const int qy0 = (int)ty * GSR_TILE_Y + (int)(quad >> 1) * 8;
+    const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
+    const bool inside = px < a.W && py < a.H;
+    const float pfx = (float)px, pfy = (float)py;
+    if (lane == 0) {
+        s_spl[64].g = make_float4(0.f, 0.f, 0.f, 0.f);
+        s_spl[64].q = make_float4(0.f, 0.f, 0.f, 0.f);
+        s_spl[64].e = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+
+    const uint2 range = a.ranges[tile];
+    // done carried in the sign of T, as in k_blend
+    float T = inside ? 1.0f : -1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
+    uint32_t last_contributor = 0;
+    auto live_any = [&]() { return __ballot(!(T <= 0.0f)) != 0ull; };
+    if (!live_any()) return;
+
+    auto composite = [&](const StagedSplat &sp) {
+        const float dx = sp.g.x - pfx, dy = sp.g.y - pfy;
+        bool vis, acc, term;
+        float test_T;
+        if (kFast) {
+            const float p2 =
+                __builtin_fmaf(dx, __builtin_fmaf(sp.g.z, dx, sp.g.w * dy), sp.q.x * dy * dy);
+            const float alpha = fminf(0.99f, sp.q.y * __builtin_amdgcn_exp2f(p2));
+            vis = !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+            const float aT = alpha * T;
+            test_T = T - aT;
+            acc = vis && !(test_T < 0.0001f);
+            term = vis && (test_T < 0.0001f);
+            const float wgt = acc ? aT : 0.0f;
+            C0 = __builtin_fmaf(sp.q.z, wgt, C0);
+            C1 = __builtin_fmaf(sp.q.w, wgt, C1);
+            C2 = __builtin_fmaf(sp.e.x, wgt, C2);
+        } else {
+            const float power =
+                -0.5f * (sp.g.z * dx * dx + sp.q.x * dy * dy) - sp.g.w * dx * dy;
+            const float alpha = fminf(0.99f, sp.q.y * exp_core(power));
+            vis = !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+            test_T = T * (1 - alpha);
+            acc = vis && !(test_T < 0.0001f);
+            term = vis && (test_T < 0.0001f);
+            C0 = acc ? C0 + sp.q.z * alpha * T : C0;
+            C1 = acc ? C1 + sp.q.w * alpha * T : C1;
+            C2 = acc ? C2 + sp.e.x * alpha * T : C2;
+        }
+        T = acc ? test_T : (term ? -fabsf(T) : T);
+        last_contributor = acc ? __float_as_uint(sp.e.y) : last_contributor;
+    };
+    const char *lds = reinterpret_cast<const char *>(s_spl);
+    auto fetch = [&](uint32_t off) { return *reinterpret_cast<const StagedSplat *>(lds + off); };
+    const float X0 = (float)qx0, Y0 = (float)qy0;
+
+    // pipeline: records of chunk c+1 and ids of chunk c+2 are in flight while c composites
+    uint32_t i0 = range.x + (uint32_t)lane;
+    uint32_t id_next = i0 + 64u < range.y ? a.point_list[i0 + 64u] : 0u;
+    SplatRecord r_next;
+    if (i0 < range.y) r_next = a.records[a.point_list[i0]];
+    for (uint32_t start = range.x; start < range.y; start += 64) {
+        const uint32_t idx = start + (uint32_t)lane;
+        const bool valid = idx < range.y;
+        const SplatRecord r = r_next;
+        if (idx + 64u < range.y) r_next = a.records[id_next];
+        if (idx + 128u < range.y) id_next = a.point_list[idx + 128u];
+
+        bool keep = valid;
+        if (valid && a.cull)
+            keep = may_touch(r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.c.y, r.c.z, 2.0f * r.c.w, X0,
+                             X0 + 7, Y0, Y0 + 7);
+        const uint64_t bal = __ballot(keep);
+        if (keep) {
+            StagedSplat st;
+            if (kFast) {
+                const float kL2e = 1.4426950408889634f;
+                st.g = make_float4(r.a.x, r.a.y, r.a.z * (-0.5f * kL2e), r.a.w * (-kL2e));
+                st.q = make_float4(r.b.x * (-0.5f * kL2e), r.b.y, r.b.z, r.b.w);
+            } else {
+                st.g = r.a;
+                st.q = r.b;
+            }
+            st.e = make_float4(r.c.x, __uint_as_float(idx - range.x + 1u), 0.0f, 0.0f);
+            const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+            const int slot = __popcll(bal & lt);  // compacted in list order
+            s_spl[slot] = st;
+        }
+        int count = __popcll(bal);
+        if (count == 0) continue;
+        // list of byte offsets, padded to an even count with the opacity-0 slot
+        if (lane < count) s_list[lane] = (uint16_t)(lane * sizeof(StagedSplat));
+        if (count & 1) {
+            if (lane == 0) s_list[count] = (uint16_t)(64 * sizeof(StagedSplat));
+            ++count;
+        }
+        // one wave: its LDS writes above complete before the reads below are served
+
+        auto next2 = [&](int k) { return k + 2 < count ? k + 2 : count - 2; };
+        StagedSplat a0 = fetch(s_list[0]), a1 = fetch(s_list[1]);
+        for (int k = 0;;) {
+            int kn = next2(k);
+            const StagedSplat b0 = fetch(s_list[kn]), b1 = fetch(s_list[kn + 1]);
+            composite(a0);
+            composite(a1);
+            k += 2;
+            if (k >= count) break;
+            kn = next2(k);
+            a0 = fetch(s_list[kn]);
+            a1 = fetch(s_list[kn + 1]);
+            composite(b0);
+            composite(b1);
+            k += 2;
+            if (k >= count) break;
+        }
+        if (!live_any()) break;
     }
 
     if (inside) {
@@ -240,11 +416,9 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
 typedef float v2f __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(128) void k_blend_fast2(const GsrBlendArgs a) {
-    __shared__ float4 s_geo[kBatch];   // x, y, prescaled conic a, b
-    __shared__ float4 s_opc[kBatch];   // prescaled conic c, opacity, r, g
-    __shared__ float s_blue[kBatch];
+    __shared__ StagedSplat s_spl[kBatch + 1];  // slot kBatch: opacity-0 pad (see k_blend)
     __shared__ uint8_t s_mask[kBatch];
-    __shared__ uint8_t s_list[2][kBatch];
+    __shared__ uint16_t s_list[2][kBatch + 1];
 
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t tx = blockIdx.x, ty_local = blockIdx.y, ty = a.row_begin + ty_local;
@@ -253,6 +427,11 @@ __global__ __launch_bounds__(128) void k_blend_fast2(const GsrBlendArgs a) {
     const bool in_a = pxa < a.W && py < a.H, in_b = pxb < a.W && py < a.H;
     const v2f pfx = {(float)pxa, (float)pxb};
     const float pfy = (float)py;
+    if (tid == 0) {
+        s_spl[kBatch].g = make_float4(0.f, 0.f, 0.f, 0.f);
+        s_spl[kBatch].q = make_float4(0.f, 0.f, 0.f, 0.f);
+        s_spl[kBatch].e = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 
     const uint2 range = a.ranges[ty_local * a.grid_x + tx];
     // done carried in the sign of T, as in k_blend
@@ -262,20 +441,20 @@ __global__ __launch_bounds__(128) void k_blend_fast2(const GsrBlendArgs a) {
     const float kL2e = 1.4426950408889634f;
     auto live_any = [&]() { return !(T.x <= 0.0f) || !(T.y <= 0.0f); };
 
-    auto composite = [&](const float4 g, const float4 q, const float blue, const uint32_t pos) {
-        const v2f dx = (v2f)g.x - pfx;
-        const float dy = g.y - pfy;
-        const v2f ady = __builtin_elementwise_fma((v2f)g.z, dx, (v2f)(g.w * dy));
-        const v2f p2 = __builtin_elementwise_fma(dx, ady, (v2f)(q.x * dy * dy));
+    auto composite = [&](const StagedSplat &sp) {
+        const v2f dx = (v2f)sp.g.x - pfx;
+        const float dy = sp.g.y - pfy;
+        const v2f ady = __builtin_elementwise_fma((v2f)sp.g.z, dx, (v2f)(sp.g.w * dy));
+        const v2f p2 = __builtin_elementwise_fma(dx, ady, (v2f)(sp.q.x * dy * dy));
         v2f e;
         e.x = __builtin_amdgcn_exp2f(p2.x);
         e.y = __builtin_amdgcn_exp2f(p2.y);
-        const v2f oe = (v2f)q.y * e;
+        const v2f oe = (v2f)sp.q.y * e;
         v2f alpha;
         alpha.x = fminf(0.99f, oe.x);
         alpha.y = fminf(0.99f, oe.y);
-        const v2f test_T = T * ((v2f)1.0f - alpha);
         const v2f aT = alpha * T;
+        const v2f test_T = T - aT;
         const bool vis_a = !(p2.x > 0.0f) && !(alpha.x < 1.0f / 255.0f);
         const bool vis_b = !(p2.y > 0.0f) && !(alpha.y < 1.0f / 255.0f);
         const bool lo_a = test_T.x < 0.0001f, lo_b = test_T.y < 0.0001f;
@@ -283,14 +462,17 @@ __global__ __launch_bounds__(128) void k_blend_fast2(const GsrBlendArgs a) {
         v2f wgt;
         wgt.x = acc_a ? aT.x : 0.0f;
         wgt.y = acc_b ? aT.y : 0.0f;
-        C0 = __builtin_elementwise_fma((v2f)q.z, wgt, C0);
-        C1 = __builtin_elementwise_fma((v2f)q.w, wgt, C1);
-        C2 = __builtin_elementwise_fma((v2f)blue, wgt, C2);
+        C0 = __builtin_elementwise_fma((v2f)sp.q.z, wgt, C0);
+        C1 = __builtin_elementwise_fma((v2f)sp.q.w, wgt, C1);
+        C2 = __builtin_elementwise_fma((v2f)sp.e.x, wgt, C2);
         T.x = acc_a ? test_T.x : ((vis_a && lo_a) ? -fabsf(T.x) : T.x);
         T.y = acc_b ? test_T.y : ((vis_b && lo_b) ? -fabsf(T.y) : T.y);
+        const uint32_t pos = __float_as_uint(sp.e.y);
         last_a = acc_a ? pos : last_a;
         last_b = acc_b ? pos : last_b;
     };
+    const char *lds = reinterpret_cast<const char *>(s_spl);
+    auto fetch = [&](uint32_t off) { return *reinterpret_cast<const StagedSplat *>(lds + off); };
 
     for (uint32_t start = range.x; start < range.y; start += kBatch) {
         if (__syncthreads_count(!live_any()) == 128) break;
@@ -308,9 +490,11 @@ __global__ __launch_bounds__(128) void k_blend_fast2(const GsrBlendArgs a) {
                     ((uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0, X0 + 7, Y0 + 8, Y0 + 15) << 2) |
                     ((uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0 + 8, X0 + 15, Y0 + 8, Y0 + 15) << 3);
             }
-            s_geo[t] = make_float4(r.a.x, r.a.y, r.a.z * (-0.5f * kL2e), r.a.w * (-kL2e));
-            s_opc[t] = make_float4(r.b.x * (-0.5f * kL2e), r.b.y, r.b.z, r.b.w);
-            s_blue[t] = r.c.x;
+            StagedSplat st;
+            st.g = make_float4(r.a.x, r.a.y, r.a.z * (-0.5f * kL2e), r.a.w * (-kL2e));
+            st.q = make_float4(r.b.x * (-0.5f * kL2e), r.b.y, r.b.z, r.b.w);
+            st.e = make_float4(r.c.x, __uint_as_float(idx - range.x + 1u), 0.0f, 0.0f);
+            s_spl[t] = st;
             s_mask[t] = (uint8_t)m;
         }
         __syncthreads();
@@ -322,29 +506,34 @@ __global__ __launch_bounds__(128) void k_blend_fast2(const GsrBlendArgs a) {
             const bool keep = j < n && ((s_mask[j] >> (2 * w)) & 3u);
             const uint64_t bal = __ballot(keep);
             const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-            if (keep) s_list[w][count + __popcll(bal & lt)] = (uint8_t)j;
+            if (keep)
+                s_list[w][count + __popcll(bal & lt)] = (uint16_t)(j * sizeof(StagedSplat));
             count += __popcll(bal);
+        }
+        if (count & 1) {
+            if (lane == 0) s_list[w][count] = (uint16_t)(kBatch * sizeof(StagedSplat));
+            ++count;
         }
         if (count == 0 || __ballot(live_any()) == 0ull) continue;
 
-        const uint32_t pos0 = start - range.x + 1u;
-        const int last = count - 1;
-        int j0 = s_list[w][0], j1 = s_list[w][min(1, last)];
-        float4 g0 = s_geo[j0], q0 = s_opc[j0], g1 = s_geo[j1], q1 = s_opc[j1];
-        float b0 = s_blue[j0], b1 = s_blue[j1];
-        for (int k = 0; k < count; k += 2) {
-            const int j2 = s_list[w][min(k + 2, last)], j3 = s_list[w][min(k + 3, last)];
-            composite(g0, q0, b0, pos0 + (uint32_t)j0);
-            g0 = s_geo[j2];
-            q0 = s_opc[j2];
-            b0 = s_blue[j2];
-            if (k + 1 < count) composite(g1, q1, b1, pos0 + (uint32_t)j1);
-            g1 = s_geo[j3];
-            q1 = s_opc[j3];
-            b1 = s_blue[j3];
-            j0 = j2;
-            j1 = j3;
-            if ((k & 30) == 30 && __ballot(live_any()) == 0ull) break;
+        const uint16_t *list = s_list[w];
+        auto next2 = [&](int k) { return k + 2 < count ? k + 2 : count - 2; };
+        StagedSplat a0 = fetch(list[0]), a1 = fetch(list[1]);
+        for (int k = 0;;) {
+            int kn = next2(k);
+            const StagedSplat b0 = fetch(list[kn]), b1 = fetch(list[kn + 1]);
+            composite(a0);
+            composite(a1);
+            k += 2;
+            if (k >= count) break;
+            kn = next2(k);
+            a0 = fetch(list[kn]);
+            a1 = fetch(list[kn + 1]);
+            composite(b0);
+            composite(b1);
+            k += 2;
+            if (k >= count) break;
+            if ((k & 28) == 0 && __ballot(live_any()) == 0ull) break;
         }
     }
 
@@ -373,9 +562,22 @@ __global__ __launch_bounds__(128) void k_blend_fast2(const GsrBlendArgs a) {
 
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s) {
     if (a.rows_tiles == 0 || a.grid_x == 0) return hipSuccess;
+    if (a.wave_quadrants && a.fast != 2) {
+        const uint32_t n_work = 4u * a.grid_x * a.rows_tiles;
+        const uint32_t per_xcd = (n_work + 7u) / 8u;
+        if (a.fast)
+            hipLaunchKernelGGL((k_blend_q<true>), dim3(8u * per_xcd), dim3(64), 0, s, a, n_work,
+                               per_xcd);
+        else
+            hipLaunchKernelGGL((k_blend_q<false>), dim3(8u * per_xcd), dim3(64), 0, s, a, n_work,
+                               per_xcd);
+        return hipGetLastError();
+    }
     const dim3 grid(a.grid_x, a.rows_tiles);
     if (a.fast == 2)
         hipLaunchKernelGGL(k_blend_fast2, grid, dim3(128), 0, s, a);
+    else if (a.fast && a.stamps)
+        hipLaunchKernelGGL((k_blend<true, true>), grid, dim3(256), 0, s, a);
     else if (a.fast)
         hipLaunchKernelGGL((k_blend<true>), grid, dim3(256), 0, s, a);
     else

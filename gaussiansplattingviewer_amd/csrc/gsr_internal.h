@@ -230,7 +230,8 @@ hipError_t gsr_launch_index_to_i32(const uint32_t *vals, int64_t P, int32_t *out
 // On return *keys / *vals point at the buffers holding the sorted data (either the input
 // pair or the alt pair).  hist needs gsr_radix_hist_words(n) words.
 int64_t gsr_radix_hist_words(int64_t n);
-// shape: tile shape (waves x items per lane): 0 = 4x16, 1 = 16x16, 2 = 4x8, 3 = 8x8, 4 = 8x16.
+// shape: tile shape (waves x items per lane): 0 = 4x16, 1 = 16x16, 2 = 4x8, 3 = 8x8, 4 = 8x16,
+// 5 = 4x4 (items per lane a multiple of 4, >= 4 waves).
 hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
                                 uint32_t **vals_alt, int64_t n, int begin_bit, int end_bit,
                                 uint32_t *hist, uint32_t *digit_total, hipStream_t s,
@@ -305,5 +306,8 @@ struct GsrBlendArgs {
     uint32_t *n_contrib;
     int cull;
     int fast;   // 1: folded-constant FMA arithmetic + raw v_exp_f32; 2: same, packed 2 px/lane
+    int wave_quadrants;  // 1: one independent wave per (tile, quadrant) (k_blend_q)
+    // diagnostics (env GSR_DEBUG_BLEND_STAMPS): per-phase s_memtime sums, see blend.hip
+    unsigned long long *stamps;
 };
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s);

@@ -45,6 +45,8 @@ __global__ __launch_bounds__(kW * 64) void k_rs_upsweep(const uint32_t *__restri
                                                         int64_t n, int shift, uint32_t mask,
                                                         uint32_t *__restrict__ hist, int64_t nb) {
     constexpr int kThreads = kW * 64, kT = kThreads * kIt;
+    static_assert(kIt % 4 == 0, "full tiles are read as uint4");
+    static_assert(kW >= 4, "the digit scans take one thread per digit (256)");
     __shared__ uint32_t s_hist[kW][kRadix];
     const int tid = threadIdx.x, w = tid >> 6;
     for (int i = tid; i < kW * kRadix; i += kThreads) (&s_hist[0][0])[i] = 0;
@@ -337,7 +339,7 @@ hipError_t gsr_launch_digit_scan(uint32_t *hist, int64_t nb, uint32_t *digit_tot
 }
 
 int64_t gsr_radix_hist_words(int64_t n) {
-    const int64_t nb = (n + 2047) / 2048;  // smallest tile shape (4 waves x 8 items)
+    const int64_t nb = (n + 1023) / 1024;  // smallest tile shape (4 waves x 4 items)
     return (nb < 1 ? 1 : nb) * kRadix;
 }
 
@@ -367,6 +369,7 @@ hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **key
             case 2: rts_pass<4, 8>(*keys, *vals, *keys_alt, *vals_alt, n, sh, nb, hist, digit_total, s); break;
             case 3: rts_pass<8, 8>(*keys, *vals, *keys_alt, *vals_alt, n, sh, nb, hist, digit_total, s); break;
             case 4: rts_pass<8, 16>(*keys, *vals, *keys_alt, *vals_alt, n, sh, nb, hist, digit_total, s); break;
+            case 5: rts_pass<4, 4>(*keys, *vals, *keys_alt, *vals_alt, n, sh, nb, hist, digit_total, s); break;
             default: rts_pass<4, 16>(*keys, *vals, *keys_alt, *vals_alt, n, sh, nb, hist, digit_total, s); break;
         }
         uint32_t *t = *keys;

@@ -146,12 +146,17 @@ const char *gsr_stage_name(int i);
  *     look-back; 0 = reduce-then-scan (identical results; faster on MI355X at these sizes,
  *     see DESIGN.md). */
 /*   GSR_OPT_TILE_SORT_SHAPE (tuning): tile shape of the pair sort's reduce-then-scan kernels,
- *     0 = 4 waves x 16 keys/lane, 1 = 16x16, 2 = 4x8, 3 = 8x8 (default), 4 = 8x16. */
+ *     0 = 4 waves x 16 keys/lane, 1 = 16x16, 2 = 4x8, 3 = 8x8 (default), 4 = 8x16, 5 = 4x4.
+ *     GSR_OPT_DEPTH_SORT_SHAPE: the same for the per-Gaussian depth sort (default 3). */
 /*   GSR_OPT_FUSED_BINNING (default 1): the pair duplication regenerates each 4096-pair chunk
  *     and performs the tile sort's first radix pass in the same kernel (reduce-then-scan
  *     sort only); 0 = separate duplicate kernel + full sort.  Identical results. */
+/*   GSR_OPT_BLEND_WAVE_QUADRANTS (default 1): the blend runs one independent wave per
+ *     (tile, 8x8 quadrant); 0 = one 4-wave block per tile with shared staging.  Identical
+ *     results.  (Ignored by GSR_OPT_BLEND_FAST = 2.) */
 enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_SORT_ONESWEEP = 3,
-       GSR_OPT_TILE_SORT_SHAPE = 4, GSR_OPT_FUSED_BINNING = 5 };
+       GSR_OPT_TILE_SORT_SHAPE = 4, GSR_OPT_FUSED_BINNING = 5, GSR_OPT_BLEND_WAVE_QUADRANTS = 6,
+       GSR_OPT_DEPTH_SORT_SHAPE = 7 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
 
 #ifdef __cplusplus

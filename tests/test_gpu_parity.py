@@ -225,19 +225,28 @@ def test_headline_config_c3(gpu, c3_oracle, fast):
     assert_parity(hip, orc)
 
 
-@pytest.mark.parametrize("variant", ["onesweep", "unfused", "shape0"])
+VARIANTS = {  # option, alternative value, default
+    "onesweep": (_lib.GSR_OPT_SORT_ONESWEEP, 1, 0),
+    "unfused": (_lib.GSR_OPT_FUSED_BINNING, 0, 1),
+    "tile_shape0": (_lib.GSR_OPT_TILE_SORT_SHAPE, 0, 3),
+    "tile_shape5": (_lib.GSR_OPT_TILE_SORT_SHAPE, 5, 3),
+    "depth_shape0": (_lib.GSR_OPT_DEPTH_SORT_SHAPE, 0, 3),
+    "depth_shape5": (_lib.GSR_OPT_DEPTH_SORT_SHAPE, 5, 3),
+    "blend_blocks": (_lib.GSR_OPT_BLEND_WAVE_QUADRANTS, 0, 1),
+}
+
+
+@pytest.mark.parametrize("variant", list(VARIANTS))
 @pytest.mark.parametrize("size", [(1920, 1080), (16, 16), (4200, 64)])
 def test_sort_implementations_agree(gpu, variant, size):
-    """The default binning (duplicate fused with the first reduce-then-scan pass) and the
-    alternatives -- onesweep sort, separate duplicate kernel, another tile shape -- give
-    identical binning and images.  Sizes: 1 tile (tbits = 0) and > 8 bits of tile id in x."""
+    """The defaults (duplicate fused with the first reduce-then-scan pass, 8x8 sort tiles, one
+    wave per blend quadrant) and the alternatives -- onesweep sort, separate duplicate
+    kernel, other sort tile shapes, 4-wave blend blocks -- give identical binning and images.  Sizes: 1 tile (tbits = 0) and > 8 bits of tile id in x."""
     w, h = size
     P = 300_000 if w * h > 10_000 else 20_000
     s = scene_inputs(synthetic_gaussians(P, 3, 21), static_camera(w, h, (0.5, 0.2, 3.5)), 3)
     ref = run_hip(s, gpu)
-    opt, val, default = {"onesweep": (_lib.GSR_OPT_SORT_ONESWEEP, 1, 0),
-                         "unfused": (_lib.GSR_OPT_FUSED_BINNING, 0, 1),
-                         "shape0": (_lib.GSR_OPT_TILE_SORT_SHAPE, 0, 3)}[variant]
+    opt, val, default = VARIANTS[variant]
     _set_option(gpu, opt, val)
     try:
         alt = run_hip(s, gpu)
