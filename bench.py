@@ -59,6 +59,8 @@ def parse():
                     help="GSR_OPT_DEPTH_SORT_SHAPE (tuning)")
     ap.add_argument("--onesweep", action="store_true", help="GSR_OPT_SORT_ONESWEEP (tuning)")
     ap.add_argument("--unfused", action="store_true", help="GSR_OPT_FUSED_BINNING=0 (tuning)")
+    ap.add_argument("--inline-color", action="store_true",
+                    help="GSR_OPT_SPLIT_COLOR=0: colour inside the preprocess kernel (tuning)")
     ap.add_argument("--blend-blocks", action="store_true",
                     help="GSR_OPT_BLEND_WAVE_QUADRANTS=0: 4-wave block per tile (tuning)")
     ap.add_argument("--blend", default="fast", choices=["exact", "fast", "packed"],
@@ -96,9 +98,11 @@ class Scene:
 
 
 def algorithmic_bytes(P, P_f, P_v, K, T, W, H, sh_bytes):
-    """algorithmic HBM bytes per stage of one frame."""
+    """algorithmic HBM bytes per stage of one frame (the SH read of the
+    preprocess is the "color" stage, which runs on the second stream)."""
     return {
-        "preprocess": 12 * P + 32 * P_f + sh_bytes * P_v + 8 * P + 40 * P_v,
+        "preprocess": 12 * P + 32 * P_f + 8 * P + 40 * P_v,
+        "color": (12 + sh_bytes) * P_v,
         "depth_sort": 16 * P,   # one read + write of (key, id) per Gaussian
         "scan": 8 * P,
         "duplicate": 4 * P + 12 * K,
@@ -168,6 +172,8 @@ def main():
         _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_TILE_SORT_SHAPE, args.sort_shape), "opt")
     if args.blend_blocks:
         _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_BLEND_WAVE_QUADRANTS, 0), "opt")
+    if args.inline_color:
+        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_SPLIT_COLOR, 0), "opt")
     if args.unfused:
         _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_FUSED_BINNING, 0), "opt")
     if args.onesweep:

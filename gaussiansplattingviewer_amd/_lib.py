@@ -21,6 +21,7 @@ GSR_OPT_TILE_SORT_SHAPE = 4
 GSR_OPT_FUSED_BINNING = 5
 GSR_OPT_BLEND_WAVE_QUADRANTS = 6
 GSR_OPT_DEPTH_SORT_SHAPE = 7
+GSR_OPT_SPLIT_COLOR = 8
 
 # Symbols include/gsr.h declares (checked by the CPU test suite).
 EXPORTED_SYMBOLS = (

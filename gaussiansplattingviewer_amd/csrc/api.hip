@@ -33,10 +33,11 @@ struct DevBuf {
     size_t cap = 0;
 };
 
-constexpr int kStages = 7;
+constexpr int kStages = 7;       // the chain on the caller's stream
+constexpr int kAllStages = 8;    // + "color", on the second stream (overlaps stages 1..5)
 constexpr int kTimingRing = 256;  // frames whose stage events are kept
-const char *kStageNames[kStages] = {"preprocess", "depth_sort", "scan",  "duplicate",
-                                    "tile_sort",  "ranges",     "blend"};
+const char *kStageNames[kAllStages] = {"preprocess", "depth_sort", "scan",  "duplicate",
+                                       "tile_sort",  "ranges",     "blend", "color"};
 
 }  // namespace
 
@@ -66,10 +67,19 @@ struct gsr_context {
     int depth_sort_shape = 3;  // 8x8: 78 us vs 89 for 4x16 at 1M keys (bench, round 1)
     int fused_binning = 1;    // duplicate fused with the first tile-sort pass
     int blend_wave_quadrants = 1;
+    int color_blocks = 512;    // grid cap of the overlapped colour pass
+    int aux_low_priority = 1;  // second stream at the lowest priority
+    bool serial_color = false; // tuning (env GSR_SERIAL_COLOR): join right after the fork
+    bool split_color = true;   // GSR_OPT_SPLIT_COLOR
     // Stage timing: a ring of event sets, one per forward, read back after the timed region.
     bool timing = false;
     int64_t timed_frames = 0;
     hipEvent_t ev[kTimingRing][kStages + 1] = {};
+    hipEvent_t ev_color[kTimingRing][2] = {};
+    // second stream: k_color runs there between a fork after the preprocess and a join
+    // before the blend
+    hipStream_t aux = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
     unsigned long long *blend_stamps = nullptr;  // diagnostics, env GSR_DEBUG_BLEND_STAMPS
 };
 
@@ -83,6 +93,7 @@ int grow(gsr_context *ctx, DevBuf &b, size_t bytes, hipStream_t s) {
     want = (want + 255) & ~size_t(255);
     if (b.p) {
         GSR_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(grow)");
+        if (ctx->aux) GSR_HIP(hipStreamSynchronize(ctx->aux), "hipStreamSynchronize(grow)");
         GSR_HIP(hipFree(b.p), "hipFree");
         b.p = nullptr;
         b.cap = 0;
@@ -93,7 +104,6 @@ int grow(gsr_context *ctx, DevBuf &b, size_t bytes, hipStream_t s) {
         return fail(GSR_E_NOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
     }
     b.cap = want;
-    (void)ctx;
     return GSR_OK;
 }
 
@@ -173,7 +183,7 @@ extern "C" {
 
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 const char *gsr_last_error(void) { return g_err.c_str(); }
-const char *gsr_stage_name(int i) { return (i >= 0 && i < kStages) ? kStageNames[i] : ""; }
+const char *gsr_stage_name(int i) { return (i >= 0 && i < kAllStages) ? kStageNames[i] : ""; }
 
 int gsr_create(gsr_context **out) {
     if (!out) return fail(GSR_E_INVALID, "gsr_create: out is NULL");
@@ -189,14 +199,29 @@ int gsr_create(gsr_context **out) {
         delete ctx;
         return fail(GSR_E_HIP, "gsr_create: hipHostMalloc failed");
     }
+    int prio_least = 0, prio_greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) {
+        (void)hipGetLastError();
+        prio_least = prio_greatest = 0;
+    }
+    const char *env_prio = std::getenv("GSR_AUX_PRIORITY");  // tuning: "0" = default priority
+    ctx->aux_low_priority = env_prio ? std::atoi(env_prio) : 1;
+    const char *env_cb = std::getenv("GSR_COLOR_BLOCKS");    // tuning: grid cap, 0 = none
+    if (env_cb) ctx->color_blocks = std::atoi(env_cb);
+    ctx->serial_color = std::getenv("GSR_SERIAL_COLOR") != nullptr;
+    bool ok = hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking,
+                                          ctx->aux_low_priority ? prio_least : 0) == hipSuccess &&
+              hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming) == hipSuccess;
     for (auto &set : ctx->ev)
-        for (auto &e : set) {
-            if (hipEventCreate(&e) != hipSuccess) {
-                (void)hipGetLastError();
-                gsr_destroy(ctx);
-                return fail(GSR_E_HIP, "gsr_create: hipEventCreate failed");
-            }
-        }
+        for (auto &e : set) ok = ok && hipEventCreate(&e) == hipSuccess;
+    for (auto &set : ctx->ev_color)
+        for (auto &e : set) ok = ok && hipEventCreate(&e) == hipSuccess;
+    if (!ok) {
+        (void)hipGetLastError();
+        gsr_destroy(ctx);
+        return fail(GSR_E_HIP, "gsr_create: stream / event creation failed");
+    }
     if (std::getenv("GSR_DEBUG_BLEND_STAMPS")) {
         if (hipMalloc(reinterpret_cast<void **>(&ctx->blend_stamps), 256 * 8 * 8) != hipSuccess ||
             hipMemset(ctx->blend_stamps, 0, 256 * 8 * 8) != hipSuccess) {
@@ -223,6 +248,12 @@ void gsr_destroy(gsr_context *ctx) {
     for (auto &set : ctx->ev)
         for (auto &e : set)
             if (e) (void)hipEventDestroy(e);
+    for (auto &set : ctx->ev_color)
+        for (auto &e : set)
+            if (e) (void)hipEventDestroy(e);
+    if (ctx->fork) (void)hipEventDestroy(ctx->fork);
+    if (ctx->join) (void)hipEventDestroy(ctx->join);
+    if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->h_total) (void)hipHostFree(ctx->h_total);
     if (ctx->blend_stamps) {
         static unsigned long long sh[256 * 8];
@@ -264,6 +295,10 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
     }
     if (option == GSR_OPT_BLEND_WAVE_QUADRANTS) {
         ctx->blend_wave_quadrants = value ? 1 : 0;
+        return GSR_OK;
+    }
+    if (option == GSR_OPT_SPLIT_COLOR) {
+        ctx->split_color = value != 0;
         return GSR_OK;
     }
     if (option == GSR_OPT_FUSED_BINNING) {
@@ -309,8 +344,17 @@ int gsr_stage_times(gsr_context *ctx, float *ms, int n) {
             acc[i] += t;
         }
     }
+    double acc_color = 0.0;
+    for (int64_t f = 0; f < frames; ++f) {
+        const int64_t slot = (ctx->timed_frames - 1 - f) % kTimingRing;
+        float t = 0.f;
+        GSR_HIP(hipEventElapsedTime(&t, ctx->ev_color[slot][0], ctx->ev_color[slot][1]),
+                "hipEventElapsedTime");
+        acc_color += t;
+    }
     for (int i = 0; i < kStages && i < n; ++i) ms[i] = (float)(acc[i] / (double)frames);
-    return kStages;
+    if (n > kStages) ms[kStages] = (float)(acc_color / (double)frames);
+    return kAllStages;
 }
 
 int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings *st,
@@ -431,7 +475,34 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     pa.tiles_touched = out->tiles_touched;
     if (pa.conic_opacity && (reinterpret_cast<uintptr_t>(pa.conic_opacity) & 15) != 0)
         return fail(GSR_E_INVALID, "gsr_forward: conic_opacity output must be 16-B aligned");
-    GSR_HIP(gsr_launch_preprocess(pa, s), "preprocess launch");
+    const bool split_color = ctx->split_color;
+    GSR_HIP(gsr_launch_preprocess(pa, !split_color, s), "preprocess launch");
+    hipEvent_t *evc = ctx->ev_color[ctx->timed_frames % kTimingRing];
+    struct JoinGuard {
+        hipStream_t s;
+        hipEvent_t join;
+        bool done = true;
+        ~JoinGuard() {
+            if (!done) (void)hipStreamWaitEvent(s, join, 0);
+        }
+    } join_guard{s, ctx->join};
+    if (split_color) {
+        // fork: colour on the second stream, overlapped with the depth sort and the binning
+        GSR_HIP(hipEventRecord(ctx->fork, s), "hipEventRecord(fork)");
+        GSR_HIP(hipStreamWaitEvent(ctx->aux, ctx->fork, 0), "hipStreamWaitEvent(fork)");
+        if (ctx->timing) GSR_HIP(hipEventRecord(evc[0], ctx->aux), "hipEventRecord");
+        GSR_HIP(gsr_launch_color(pa, ctx->color_blocks, ctx->aux), "color launch");
+        if (ctx->timing) GSR_HIP(hipEventRecord(evc[1], ctx->aux), "hipEventRecord");
+        GSR_HIP(hipEventRecord(ctx->join, ctx->aux), "hipEventRecord(join)");
+        // every exit from here on (errors included) leaves the caller's stream behind the
+        // join, so k_color never outlives the caller's view of its inputs
+        join_guard.done = false;
+        if (dbg) GSR_HIP(hipStreamSynchronize(ctx->aux), "stage color");
+        if (ctx->serial_color) GSR_HIP(hipStreamWaitEvent(s, ctx->join, 0), "hipStreamWaitEvent");
+    } else if (ctx->timing) {  // no colour stage: record an empty interval
+        GSR_HIP(hipEventRecord(evc[0], s), "hipEventRecord");
+        GSR_HIP(hipEventRecord(evc[1], s), "hipEventRecord");
+    }
     GSR_TRY(stage_end(0));
 
     // ---- 2. stable radix sort of the Gaussians by view depth ------------------------------
@@ -543,6 +614,10 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     ba.fast = ctx->fast;
     ba.wave_quadrants = ctx->blend_wave_quadrants;
     ba.stamps = ctx->blend_stamps;
+    if (!join_guard.done) {
+        join_guard.done = true;
+        GSR_HIP(hipStreamWaitEvent(s, ctx->join, 0), "hipStreamWaitEvent(join)");
+    }
     GSR_HIP(gsr_launch_blend(ba, s), "blend launch");
     GSR_TRY(stage_end(6));
 

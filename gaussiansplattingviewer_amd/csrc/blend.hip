@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
             uint32_t m = 0xF;
             if (a.cull) {
                 const float x = r.a.x, y = r.a.y, A = r.a.z, B = r.a.w, C = r.b.x;
-                const float ex = r.c.y, ey = r.c.z, twoL = 2.0f * r.c.w;
+                const float ex = r.b.z, ey = r.b.w, twoL = 2.0f * r.c.x;
                 const float X0 = (float)tx0, Y0 = (float)ty0;
                 m = (uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0, X0 + 7, Y0, Y0 + 7) |
                     ((uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0 + 8, X0 + 15, Y0, Y0 + 7) << 1) |
@@ -170,12 +170,12 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
             if (kFast) {
                 const float kL2e = 1.4426950408889634f;
                 st.g = make_float4(r.a.x, r.a.y, r.a.z * (-0.5f * kL2e), r.a.w * (-kL2e));
-                st.q = make_float4(r.b.x * (-0.5f * kL2e), r.b.y, r.b.z, r.b.w);
+                st.q = make_float4(r.b.x * (-0.5f * kL2e), r.b.y, r.c.y, r.c.z);
             } else {
                 st.g = r.a;
-                st.q = r.b;
+                st.q = make_float4(r.b.x, r.b.y, r.c.y, r.c.z);
             }
-            st.e = make_float4(r.c.x, __uint_as_float(idx - range.x + 1u), 0.0f, 0.0f);
+            st.e = make_float4(r.c.w, __uint_as_float(idx - range.x + 1u), 0.0f, 0.0f);
             s_spl[tid] = st;
             s_mask[tid] = (uint8_t)m;
         }
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(64) void k_blend_q(const GsrBlendArgs a, uint32_t n
 
         bool keep = valid;
         if (valid && a.cull)
-            keep = may_touch(r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.c.y, r.c.z, 2.0f * r.c.w, X0,
+            keep = may_touch(r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.z, r.b.w, 2.0f * r.c.x, X0,
                              X0 + 7, Y0, Y0 + 7);
         const uint64_t bal = __ballot(keep);
         if (keep) {
@@ -356,12 +356,12 @@ __global__ __launch_bounds__(64) void k_blend_q(const GsrBlendArgs a, uint32_t n
             if (kFast) {
                 const float kL2e = 1.4426950408889634f;
                 st.g = make_float4(r.a.x, r.a.y, r.a.z * (-0.5f * kL2e), r.a.w * (-kL2e));
-                st.q = make_float4(r.b.x * (-0.5f * kL2e), r.b.y, r.b.z, r.b.w);
+                st.q = make_float4(r.b.x * (-0.5f * kL2e), r.b.y, r.c.y, r.c.z);
             } else {
                 st.g = r.a;
-                st.q = r.b;
+                st.q = make_float4(r.b.x, r.b.y, r.c.y, r.c.z);
             }
-            st.e = make_float4(r.c.x, __uint_as_float(idx - range.x + 1u), 0.0f, 0.0f);
+            st.e = make_float4(r.c.w, __uint_as_float(idx - range.x + 1u), 0.0f, 0.0f);
             const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
             const int slot = __popcll(bal & lt);  // compacted in list order
             s_spl[slot] = st;
@@ -483,7 +483,7 @@ __global__ __launch_bounds__(128) void k_blend_fast2(const GsrBlendArgs a) {
             uint32_t m = 0xF;
             if (a.cull) {
                 const float x = r.a.x, y = r.a.y, A = r.a.z, B = r.a.w, C = r.b.x;
-                const float ex = r.c.y, ey = r.c.z, twoL = 2.0f * r.c.w;
+                const float ex = r.b.z, ey = r.b.w, twoL = 2.0f * r.c.x;
                 const float X0 = (float)tx0, Y0 = (float)ty0;
                 m = (uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0, X0 + 7, Y0, Y0 + 7) |
                     ((uint32_t)may_touch(x, y, A, B, C, ex, ey, twoL, X0 + 8, X0 + 15, Y0, Y0 + 7) << 1) |
@@ -492,8 +492,8 @@ __global__ __launch_bounds__(128) void k_blend_fast2(const GsrBlendArgs a) {
             }
             StagedSplat st;
             st.g = make_float4(r.a.x, r.a.y, r.a.z * (-0.5f * kL2e), r.a.w * (-kL2e));
-            st.q = make_float4(r.b.x * (-0.5f * kL2e), r.b.y, r.b.z, r.b.w);
-            st.e = make_float4(r.c.x, __uint_as_float(idx - range.x + 1u), 0.0f, 0.0f);
+            st.q = make_float4(r.b.x * (-0.5f * kL2e), r.b.y, r.c.y, r.c.z);
+            st.e = make_float4(r.c.w, __uint_as_float(idx - range.x + 1u), 0.0f, 0.0f);
             s_spl[t] = st;
             s_mask[t] = (uint8_t)m;
         }

@@ -17,10 +17,10 @@
 
 namespace gsr {
 
-// One visible Gaussian as the blend consumes it: 48 B, three 16-B loads, written by the
-// preprocess, gathered by tile lists.  a = {x, y, conic.a, conic.b}; b = {conic.c, opacity,
-// r, g}; c = {b, cull_ex, cull_ey, cull_Lm} (conservative alpha >= 1/255 region, see
-// preprocess.hip cull_data).
+// One visible Gaussian as the blend consumes it: 48 B, three 16-B loads, gathered by tile
+// lists.  a = {x, y, conic.a, conic.b}; b = {conic.c, opacity, cull_ex, cull_ey}; c = {cull_Lm,
+// r, g, b} (cull_*: conservative alpha >= 1/255 region, see preprocess.hip cull_data).
+// k_preprocess writes a, b and c.x; k_color writes the colour c.yzw (on the second stream).
 struct alignas(16) SplatRecord {
     float4 a, b, c;
 };
@@ -218,7 +218,11 @@ struct GsrPreprocessArgs {
     uint32_t *tiles_touched;
 };
 
-hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, hipStream_t s);
+// with_color: evaluate the colour in the same kernel (else gsr_launch_color does it)
+hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, bool with_color, hipStream_t s);
+// SH -> RGB (or colors_precomp) of every Gaussian with radii > 0 into SplatRecord.c.yzw (+ rgb)
+// max_blocks > 0 caps the grid (grid-stride loop).
+hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, hipStream_t s);
 hipError_t gsr_launch_mark_visible(const float *means3D, int64_t P, const float *viewmatrix,
                                    uint8_t *visible, hipStream_t s);
 hipError_t gsr_launch_view_depth_keys(const float *xyz, int64_t P, float v20, float v21, float v22,

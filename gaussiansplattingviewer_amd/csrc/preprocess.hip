@@ -2,12 +2,15 @@
 //
 // Replaces upstream diff-gaussian-rasterization forward.cu preprocessCUDA (called from
 // renderer_cuda.py:215 via GaussianRasterizer.forward) and auxiliary.h in_frustum.
-// One thread per Gaussian, 256-thread blocks (4 waves).  HBM-bound: per Gaussian it reads
-// xyz (12 B) for every point, scale/rot/opacity (32 B) for points in front of the camera
-// and SH (192 B at degree 3) only for points that survive culling; it writes one 48-B
-// SplatRecord for visible points plus the 8-B (key, id) pair of the depth sort and 8 B of
-// radius / strip tile count.  SplatRecord: a = {x, y, conic.a, conic.b}, b = {conic.c,
-// opacity, r, g}, c = {b, cull ex, cull ey, cull Lm}.
+// Two kernels, one thread per Gaussian, 256-thread blocks:
+//  * k_preprocess -- projection, covariance, conic, radius, tile rect, depth key: reads xyz
+//    (12 B) for every point and scale/rot/opacity (32 B) for points in front of the camera;
+//    writes the geometry of the 48-B SplatRecord for visible points, the 8-B (key, id) pair
+//    of the depth sort, the radius and the packed strip rect.
+//  * k_color -- SH -> RGB for the visible points: reads xyz + SH (192 B at degree 3), writes
+//    the record's colour.  It depends only on k_preprocess's radii and nothing before the
+//    blend reads colour, so api.hip runs it on a second stream, overlapped with the depth
+//    sort and the binning (which are latency-bound and leave most CUs idle).
 #include "gsr_internal.h"
 
 using namespace gsr;
@@ -25,13 +28,11 @@ __constant__ float kShC3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
 // upstream forward.cu computeColorFromSH (twin: shaders/gau_vert.glsl:213-250), but with the
 // coefficients read as 16-B vectors: the (P, M, 3) row of one Gaussian is 192 B = 12 float4
 // at degree 3 (M = 16), so each lane issues 12 dwordx4 loads instead of 48 dword loads.
+__device__ __forceinline__ float3 eval_sh(float3 pos, const float *campos, const float (&c)[48],
+                                          int deg);
+
 __device__ __forceinline__ float3 color_from_sh(float3 pos, const float *campos, const float *sh,
                                                 int deg, bool vec_ok) {
-    float dx = pos.x - campos[0], dy = pos.y - campos[1], dz = pos.z - campos[2];
-    const float len = sqrtf(dx * dx + dy * dy + dz * dz);
-    dx = dx / len;
-    dy = dy / len;
-    dz = dz / len;
     // Load the coefficients this degree needs: (deg+1)^2 of the M stored (host checks
     // (deg+1)^2 <= M).  Both loops are fully unrolled so `c` stays in registers.
     float c[48];
@@ -53,6 +54,16 @@ __device__ __forceinline__ float3 color_from_sh(float3 pos, const float *campos,
 #pragma unroll
         for (int i = 0; i < 48; ++i) c[i] = (i < nflt) ? sh[i] : 0.0f;
     }
+    return eval_sh(pos, campos, c, deg);
+}
+
+__device__ __forceinline__ float3 eval_sh(float3 pos, const float *campos, const float (&c)[48],
+                                          int deg) {
+    float dx = pos.x - campos[0], dy = pos.y - campos[1], dz = pos.z - campos[2];
+    const float len = sqrtf(dx * dx + dy * dy + dz * dz);
+    dx = dx / len;
+    dy = dy / len;
+    dz = dz / len;
     float r0 = kShC0 * c[0], r1 = kShC0 * c[1], r2 = kShC0 * c[2];
     if (deg > 0) {
         const float x = dx, y = dy, z = dz;
@@ -120,6 +131,8 @@ __device__ __forceinline__ float3 cull_data(float A, float B, float C, float o) 
     return make_float3((float)ex, (float)ey, __uint_as_float(__float_as_uint((float)Lm) + 1u));
 }
 
+// kColor: also evaluate the colour here (one kernel, no second stream).
+template <bool kColor>
 __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= a.P) return;
@@ -164,13 +177,6 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
             const Rect rc = get_rect(px, py, r_int, a.grid_x, a.grid_y);
             all_tiles = (rc.x1 - rc.x0) * (rc.y1 - rc.y0);
             if (all_tiles != 0) {
-                float3 col;
-                if (a.colors_precomp) {
-                    col = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1],
-                                      a.colors_precomp[3 * idx + 2]);
-                } else {
-                    col = color_from_sh(p, a.campos, a.shs + idx * (int64_t)a.M * 3, a.D, a.sh_vec4);
-                }
                 const float opacity = a.opacities[idx];
                 radius_out = r_int;
                 const uint32_t sy0 = max(rc.y0, a.row_begin), sy1 = min(rc.y1, a.row_end);
@@ -180,11 +186,27 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
                                             (sy0 - a.row_begin) | ((sy1 - sy0) << 16));
                 if (strip_tiles) key = __float_as_uint(p_view.z);  // z > 0.2: bits are monotone
                 const float3 cd = cull_data(conic_a, conic_b, conic_c, opacity);
-                SplatRecord rec;
+                SplatRecord &rec = a.records[idx];
                 rec.a = make_float4(px, py, conic_a, conic_b);
-                rec.b = make_float4(conic_c, opacity, col.x, col.y);
-                rec.c = make_float4(col.z, cd.x, cd.y, cd.z);
-                a.records[idx] = rec;
+                rec.b = make_float4(conic_c, opacity, cd.x, cd.y);
+                if (kColor) {
+                    float3 col;
+                    if (a.colors_precomp) {
+                        col = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1],
+                                          a.colors_precomp[3 * idx + 2]);
+                    } else {
+                        col = color_from_sh(p, a.campos, a.shs + idx * (int64_t)a.M * 3, a.D,
+                                            a.sh_vec4);
+                        if (a.rgb) {
+                            a.rgb[3 * idx] = col.x;
+                            a.rgb[3 * idx + 1] = col.y;
+                            a.rgb[3 * idx + 2] = col.z;
+                        }
+                    }
+                    rec.c = make_float4(cd.z, col.x, col.y, col.z);
+                } else {
+                    rec.c.x = cd.z;  // c.yzw: colour, written by k_color
+                }
                 if (a.depths) a.depths[idx] = p_view.z;
                 if (a.means2D) {
                     a.means2D[2 * idx] = px;
@@ -193,11 +215,6 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
                 if (a.conic_opacity)
                     reinterpret_cast<float4 *>(a.conic_opacity)[idx] =
                         make_float4(conic_a, conic_b, conic_c, opacity);
-                if (a.rgb && !a.colors_precomp) {
-                    a.rgb[3 * idx] = col.x;
-                    a.rgb[3 * idx + 1] = col.y;
-                    a.rgb[3 * idx + 2] = col.z;
-                }
             }
         }
     }
@@ -206,6 +223,87 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
     a.sort_keys[idx] = key;
     a.sort_vals[idx] = (uint32_t)idx;
     if (a.tiles_touched) a.tiles_touched[idx] = strip_tiles;
+}
+
+// Colour of the Gaussians k_preprocess kept (radii > 0, as upstream computes colour only for
+// those): upstream computeColorFromSH, or colors_precomp copied.
+__device__ __forceinline__ void color_one(const GsrPreprocessArgs &a, int64_t idx) {
+    if (a.radii[idx] == 0) return;
+    float3 col;
+    if (a.colors_precomp) {
+        col = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1],
+                          a.colors_precomp[3 * idx + 2]);
+    } else {
+        const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1],
+                                     a.means3D[3 * idx + 2]);
+        col = color_from_sh(p, a.campos, a.shs + idx * (int64_t)a.M * 3, a.D, a.sh_vec4);
+        if (a.rgb) {
+            a.rgb[3 * idx] = col.x;
+            a.rgb[3 * idx + 1] = col.y;
+            a.rgb[3 * idx + 2] = col.z;
+        }
+    }
+    float *c = &a.records[idx].c.x;
+    c[1] = col.x;
+    c[2] = col.y;
+    c[3] = col.z;
+}
+
+// Grid-stride over waves of 64 Gaussians; the grid is capped (api.hip) so the colour pass,
+// which runs beside the latency-bound depth sort, leaves CUs free for it.  With 16-B aligned
+// degree-3 rows (M = 16, a.sh_vec4) a wave reads its 64 rows -- 12 KiB, contiguous -- with
+// fully coalesced 16-B loads (lane l takes float4 i*64 + l), transposes them through LDS
+// (rows padded to 13 float4 so the per-lane 16-B reads are bank-conflict free) and each lane
+// evaluates its own row; rows of invisible Gaussians are skipped when the whole wave is
+// invisible.  Otherwise every lane reads its own row (color_from_sh).
+constexpr int kShRowPad = 13;  // float4 per LDS row
+__global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
+    __shared__ float4 s_sh[4][64 * kShRowPad];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t n_waves = (a.P + 63) / 64;
+    const int64_t wave_stride = (int64_t)gridDim.x * 4;
+    for (int64_t wv = (int64_t)blockIdx.x * 4 + w; wv < n_waves; wv += wave_stride) {
+        const int64_t base = wv * 64, idx = base + lane;
+        const bool in = idx < a.P;
+        const bool vis = in && a.radii[idx] != 0;
+        if (__ballot(vis) == 0ull) continue;
+        if (!a.sh_vec4 || a.colors_precomp || a.D != 3) {
+            if (vis) color_one(a, idx);
+            continue;
+        }
+        const float4 *rows = reinterpret_cast<const float4 *>(a.shs) + base * 12;
+        const int64_t n_vec = min<int64_t>(64, a.P - base) * 12;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+            const int v = i * 64 + lane;  // float4 v of the wave's rows: row v / 12, col v % 12
+            if (v < n_vec) s_sh[w][(v / 12) * kShRowPad + v % 12] = rows[v];
+        }
+        // one wave: its LDS writes complete before its reads below
+        if (vis) {
+            float c[48];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) {
+                const float4 q = s_sh[w][lane * kShRowPad + i];
+                c[4 * i + 0] = q.x;
+                c[4 * i + 1] = q.y;
+                c[4 * i + 2] = q.z;
+                c[4 * i + 3] = q.w;
+            }
+            const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1],
+                                         a.means3D[3 * idx + 2]);
+            const float3 col = eval_sh(p, a.campos, c, 3);
+            if (a.rgb) {
+                a.rgb[3 * idx] = col.x;
+                a.rgb[3 * idx + 1] = col.y;
+                a.rgb[3 * idx + 2] = col.z;
+            }
+            float *cc = &a.records[idx].c.x;
+            cc[1] = col.x;
+            cc[2] = col.y;
+            cc[3] = col.z;
+        }
+        // the next iteration's LDS writes follow this wave's reads in order
+    }
 }
 
 // GaussianRasterizer.markVisible -> upstream markVisible kernel: in_frustum only.
@@ -245,9 +343,20 @@ inline unsigned grid_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace
 
-hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, hipStream_t s) {
+hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, bool with_color, hipStream_t s) {
     if (a.P == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_preprocess, dim3(grid_for(a.P)), dim3(256), 0, s, a);
+    if (with_color)
+        hipLaunchKernelGGL(k_preprocess<true>, dim3(grid_for(a.P)), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_preprocess<false>, dim3(grid_for(a.P)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, hipStream_t s) {
+    if (a.P == 0) return hipSuccess;
+    const unsigned g = grid_for(a.P);  // 4 waves of 64 Gaussians per block
+    hipLaunchKernelGGL(k_color, dim3(max_blocks > 0 && (unsigned)max_blocks < g ? max_blocks : g),
+                       dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -154,9 +154,12 @@ const char *gsr_stage_name(int i);
 /*   GSR_OPT_BLEND_WAVE_QUADRANTS (default 1): the blend runs one independent wave per
  *     (tile, 8x8 quadrant); 0 = one 4-wave block per tile with shared staging.  Identical
  *     results.  (Ignored by GSR_OPT_BLEND_FAST = 2.) */
+/*   GSR_OPT_SPLIT_COLOR (default 1): SH -> RGB runs as its own kernel on an internal second
+ *     stream, overlapped with the depth sort and the binning; 0 = inside the preprocess
+ *     kernel.  Identical results. */
 enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_SORT_ONESWEEP = 3,
        GSR_OPT_TILE_SORT_SHAPE = 4, GSR_OPT_FUSED_BINNING = 5, GSR_OPT_BLEND_WAVE_QUADRANTS = 6,
-       GSR_OPT_DEPTH_SORT_SHAPE = 7 };
+       GSR_OPT_DEPTH_SORT_SHAPE = 7, GSR_OPT_SPLIT_COLOR = 8 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
 
 #ifdef __cplusplus

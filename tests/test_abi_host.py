@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
     assert lib.gsr_abi_version() == _lib.ABI_VERSION
     assert _lib.stage_names() == ["preprocess", "depth_sort", "scan", "duplicate", "tile_sort",
-                                  "ranges", "blend"]
+                                  "ranges", "blend", "color"]
 
 
 def test_library_is_gfx950_code_object():

@@ -233,6 +233,7 @@ VARIANTS = {  # option, alternative value, default
     "depth_shape0": (_lib.GSR_OPT_DEPTH_SORT_SHAPE, 0, 3),
     "depth_shape5": (_lib.GSR_OPT_DEPTH_SORT_SHAPE, 5, 3),
     "blend_blocks": (_lib.GSR_OPT_BLEND_WAVE_QUADRANTS, 0, 1),
+    "inline_color": (_lib.GSR_OPT_SPLIT_COLOR, 0, 1),
 }
 
 
