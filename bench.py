@@ -97,6 +97,26 @@ class Scene:
                                           tile_rows=tile_rows)
 
 
+# Measured HBM traffic per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate PMC passes;
+# tools/profile.sh + tools/prof_summary.py --json) of the default configuration, and the kernel
+# each stage's roofline refers to.  The bench cannot read PMC counters itself; the profile is
+# of this same command (c3, default options).
+TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r01_c3_v6_kernels.json")
+STAGE_KERNEL = {"blend": "k_blend_q<true>", "preprocess": "k_preprocess<false>",
+                "color": "k_color", "depth_sort": None, "duplicate": "k_dup_scatter",
+                "tile_sort": None, "scan": None, "ranges": "k_ranges"}
+
+
+def measured_traffic(stage, config, default_opts):
+    if config != "c3" or not default_opts or not os.path.exists(TRAFFIC_PROFILE):
+        return None, None
+    k = STAGE_KERNEL.get(stage)
+    rec = json.load(open(TRAFFIC_PROFILE)).get(k) if k else None
+    if not rec or rec.get("read_bytes_x2") is None or rec.get("write_bytes") is None:
+        return None, None
+    return int(rec["read_bytes_x2"] + rec["write_bytes"]), os.path.relpath(TRAFFIC_PROFILE, REPO)
+
+
 def algorithmic_bytes(P, P_f, P_v, K, T, W, H, sh_bytes):
     """algorithmic HBM bytes per stage of one frame (the SH read of the
     preprocess is the "color" stage, which runs on the second stream)."""
@@ -224,6 +244,10 @@ def main():
     dominant = max(stage_ms, key=stage_ms.get)
     ach = alg[dominant] / (stage_ms[dominant] * 1e-3) / 1e9
 
+    default_opts = not (args.sort_shape is not None or args.depth_sort_shape is not None or
+                        args.onesweep or args.unfused or args.blend_blocks or args.inline_color or
+                        args.blend != "fast")
+    traffic, traffic_src = measured_traffic(dominant, args.config, default_opts)
     fps = args.steps / t_max
     line = {
         "metric": METRIC,
@@ -249,7 +273,8 @@ def main():
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                     "traffic": None,
+                     "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "bytes_per_launch": int(alg[dominant]),
                      "frame_achieved_gbs": round(sum(alg.values()) / (1e-3 * sum(stage_ms.values())) / 1e9, 2)},
         "cpu_baseline": None,

@@ -60,6 +60,7 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--out")
     ap.add_argument("--title", default="")
+    ap.add_argument("--json", help="also write per-kernel {avg_us, read_bytes_x2, write_bytes}")
     a = ap.parse_args()
     stats = load_stats(a.dir)
     fetch = load_pmc(a.dir, "FETCH_SIZE")
@@ -77,7 +78,20 @@ def main():
         wmb = sum(w) / len(w) * 1024 / 1e6 if w else float("nan")
         lines.append(f"| {k} | {calls} | {avg / 1e3:.2f} | {100 * tot / total:.1f}% | {fmb:.2f} | "
                      f"{2 * fmb:.2f} | {wmb:.2f} |")
+    lines += ["", "FETCH/WRITE are per launch, averaged over the launches of the PMC passes; "
+              "`read MB x2-corr` doubles FETCH_SIZE per the gfx950 calibration (wide coalesced "
+              "reads); other access widths are uncalibrated."]
     text = "\n".join(lines) + "\n"
+    if a.json:
+        import json
+        out = {}
+        for k, (calls, avg, tot) in stats.items():
+            f, w = fetch.get(k), write.get(k)
+            out[k] = {"calls": calls, "avg_us": avg / 1e3,
+                      "read_bytes_x2": 2 * sum(f) / len(f) * 1024 if f else None,
+                      "write_bytes": sum(w) / len(w) * 1024 if w else None}
+        os.makedirs(os.path.dirname(a.json) or ".", exist_ok=True)
+        json.dump(out, open(a.json, "w"), indent=1, sort_keys=True)
     print(text)
     if a.out:
         os.makedirs(os.path.dirname(a.out), exist_ok=True)
