@@ -45,7 +45,7 @@ struct gsr_context {
     int device = 0;
     // per-Gaussian workspace
     DevBuf records, strip_rect, sort_keys, sort_vals, sort_keys_alt, sort_vals_alt, partials,
-        total, hist, digit_total, bin, chunk_first;
+        total, hist, digit_total, bin, chunk_first, rect_sorted;
     // onesweep sort state: [0,1024) depth-sort digit counts, [1024,2048) tile-sort counts,
     // then the ticket word; look-back granules
     DevBuf sort_ctl, status;
@@ -135,6 +135,7 @@ int reserve_P(gsr_context *ctx, int64_t P, hipStream_t s) {
     GSR_TRY(grow(ctx, ctx->hist, (size_t)gsr_radix_hist_words(P) * 4, s));
     GSR_TRY(grow(ctx, ctx->digit_total, 256 * 4, s));
     GSR_TRY(grow(ctx, ctx->bin, n * 16, s));
+    GSR_TRY(grow(ctx, ctx->rect_sorted, n * 8, s));
     GSR_TRY(grow_zeroed(ctx, ctx->sort_ctl, 2048 * 4 + 256, s));
     GSR_TRY(grow_zeroed(ctx, ctx->status, (size_t)gsr_onesweep_status_words(P) * 8, s));
     return GSR_OK;
@@ -240,6 +241,7 @@ void gsr_destroy(gsr_context *ctx) {
                       &ctx->sort_vals,     &ctx->sort_keys_alt, &ctx->sort_vals_alt,
                       &ctx->partials,      &ctx->total,         &ctx->hist,
                       &ctx->digit_total,   &ctx->bin,           &ctx->chunk_first,
+                      &ctx->rect_sorted,
                       &ctx->sort_ctl,      &ctx->status,
                       &ctx->tile_keys,     &ctx->tile_vals,
                       &ctx->tile_keys_alt, &ctx->tile_vals_alt, &ctx->ranges_local};
@@ -529,7 +531,9 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     // ---- 3. offsets scan over depth-sorted strip tile counts; K readback --------------------
     uint32_t *partials = static_cast<uint32_t *>(ctx->partials.p);
     uint64_t *d_total = static_cast<uint64_t *>(ctx->total.p);
-    GSR_HIP(gsr_launch_scan_reduce(perm, pa.strip_rect, P, partials, s), "scan launch");
+    uint2 *rect_sorted = static_cast<uint2 *>(ctx->rect_sorted.p);
+    GSR_HIP(gsr_launch_scan_reduce(perm, pa.strip_rect, P, partials, rect_sorted, s),
+            "scan launch");
     GSR_HIP(gsr_launch_scan_partials(partials, gsr_scan_blocks(P), d_total, s), "scan launch");
     GSR_HIP(hipMemcpyAsync(ctx->h_total, d_total, 16, hipMemcpyDeviceToHost, s),
             "hipMemcpyAsync(num_rendered)");
@@ -554,7 +558,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     const GsrRadixPlan tplan = gsr_radix_plan(0, tbits);
     const bool fused = !ctx->onesweep && ctx->fused_binning;
     if (K > 0) {
-        GSR_HIP(gsr_launch_scan_down(perm, pa.strip_rect, partials, P, d_total, bin, chunk_first,
+        GSR_HIP(gsr_launch_scan_down(perm, rect_sorted, partials, P, d_total, bin, chunk_first,
                                      s),
                 "scan_down launch");
         if (fused) {
@@ -562,7 +566,9 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
             GSR_HIP(gsr_launch_dup_sort_pass(bin, chunk_first, (int64_t)K, gx,
                                              tplan.n ? tplan.shift[0] : 0,
                                              tplan.n ? tplan.nbits[0] : 0, hist, digit_total,
-                                             tk_alt, tv_alt, s),
+                                             tk_alt, tv_alt,
+                                             static_cast<uint2 *>(ctx->ranges_local.p),
+                                             (uint32_t)T_strip, s),
                     "duplicate launch");
             std::swap(tk, tk_alt);
             std::swap(tv, tv_alt);
@@ -589,7 +595,8 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     GSR_TRY(stage_end(4));
 
     // ---- 6. tile ranges ----------------------------------------------------------------------
-    GSR_HIP(hipMemsetAsync(ctx->ranges_local.p, 0, T_strip * 8, s), "hipMemsetAsync(ranges)");
+    if (!(fused && K > 0))  // else zeroed by k_dup_count
+        GSR_HIP(hipMemsetAsync(ctx->ranges_local.p, 0, T_strip * 8, s), "hipMemsetAsync(ranges)");
     GSR_HIP(gsr_launch_ranges(tk, (int64_t)K, static_cast<uint32_t *>(ctx->ranges_local.p), s),
             "ranges launch");
     GSR_TRY(stage_end(5));

@@ -20,19 +20,26 @@ constexpr int kItems = 4;
 constexpr int kTile = kBlock * kItems;  // 1024 depth-sorted Gaussians per scan block
 constexpr uint32_t kChunk = 2048;        // output pairs per duplicate block
 
-// Pass 1 of the scan: per-block sum of the strip tile counts, gathered in depth order.
+// Pass 1 of the scan: per-block sum of the strip tile counts, gathered in depth order; the
+// gathered rects are also written out in depth order (rect_sorted) so pass 3 reads them
+// coalesced instead of gathering them a second time.
 __device__ __forceinline__ uint32_t rect_count(uint2 r) { return (r.x >> 16) * (r.y >> 16); }
 
 __global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t *__restrict__ perm,
                                                         const uint2 *__restrict__ strip_rect,
-                                                        int64_t n, uint32_t *__restrict__ partials) {
+                                                        int64_t n, uint32_t *__restrict__ partials,
+                                                        uint2 *__restrict__ rect_sorted) {
     __shared__ uint32_t s_tmp[4];
     const int64_t base = (int64_t)blockIdx.x * kTile;
     uint32_t sum = 0;
 #pragma unroll 4
     for (int j = 0; j < kItems; ++j) {
         const int64_t e = base + j * kBlock + threadIdx.x;
-        if (e < n) sum += rect_count(strip_rect[perm[e]]);
+        if (e < n) {
+            const uint2 r = strip_rect[perm[e]];
+            rect_sorted[e] = r;
+            sum += rect_count(r);
+        }
     }
     uint32_t total;
     block256_exclusive_scan(sum, s_tmp, total);
@@ -63,7 +70,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_partials(uint32_t *__restrict__
 // chunk_first[n_chunks] = one past the last Gaussian with pairs.  Gaussians without pairs in
 // the strip carry the sentinel depth key, so they all sit after the last non-empty one.
 __global__ __launch_bounds__(kBlock) void k_scan_down(const uint32_t *__restrict__ perm,
-                                                      const uint2 *__restrict__ strip_rect,
+                                                      const uint2 *__restrict__ rect_sorted,
                                                       const uint32_t *__restrict__ partials,
                                                       int64_t n, const uint64_t *__restrict__ total,
                                                       uint4 *__restrict__ bin,
@@ -77,7 +84,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_down(const uint32_t *__restrict
     for (int j = 0; j < kItems; ++j) {
         const int64_t e = base + j;
         id[j] = e < n ? perm[e] : 0u;
-        rc[j] = e < n ? strip_rect[id[j]] : make_uint2(0u, 0u);
+        rc[j] = e < n ? rect_sorted[e] : make_uint2(0u, 0u);
         cnt[j] = rect_count(rc[j]);
         sum += cnt[j];
     }
@@ -279,8 +286,11 @@ __device__ __forceinline__ void gen_pairs(const DupStage &st, bool staged, const
 __global__ __launch_bounds__(kFW * 64) void k_dup_count(
     const uint4 *__restrict__ bin, const uint32_t *__restrict__ chunk_first, uint32_t K,
     uint32_t n_chunks, uint32_t gx, int shift, uint32_t mask, uint32_t *__restrict__ hist,
-    int64_t nb) {
+    int64_t nb, uint2 *__restrict__ ranges_zero, uint32_t n_ranges) {
     __shared__ DupStage st;
+    // zero the tile ranges for k_ranges (saves a memset launch)
+    for (uint32_t i = blockIdx.x * (kFW * 64) + threadIdx.x; i < n_ranges; i += gridDim.x * (kFW * 64))
+        ranges_zero[i] = make_uint2(0u, 0u);
     __shared__ uint32_t s_h[kFW][kRadixBins];
     const int tid = threadIdx.x, w = tid >> 6;
     const uint32_t c = blockIdx.x;
@@ -349,21 +359,37 @@ __global__ __launch_bounds__(kFW * 64) void k_dup_scatter(
 }
 
 // upstream identifyTileRanges over the tile-sorted keys (ranges pre-zeroed).
+// 4 keys per thread (one 16-B load when aligned and complete).
 __global__ __launch_bounds__(kBlock) void k_ranges(const uint32_t *__restrict__ tile_keys,
                                                    int64_t K, uint32_t *__restrict__ ranges) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= K) return;
-    const uint32_t cur = tile_keys[i];
-    if (i == 0) {
-        ranges[2 * cur] = 0;
+    const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
+    if (i0 >= K) return;
+    uint32_t k[4];
+    if (i0 + 4 <= K) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(tile_keys + i0);
+        k[0] = q.x;
+        k[1] = q.y;
+        k[2] = q.z;
+        k[3] = q.w;
     } else {
-        const uint32_t prev = tile_keys[i - 1];
-        if (cur != prev) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) k[j] = i0 + j < K ? tile_keys[i0 + j] : 0u;
+    }
+    uint32_t prev = i0 > 0 ? tile_keys[i0 - 1] : 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int64_t i = i0 + j;
+        if (i >= K) break;
+        const uint32_t cur = k[j];
+        if (i == 0) {
+            ranges[2 * cur] = 0;
+        } else if (cur != prev) {
             ranges[2 * prev + 1] = (uint32_t)i;
             ranges[2 * cur] = (uint32_t)i;
         }
+        if (i == K - 1) ranges[2 * cur + 1] = (uint32_t)K;
+        prev = cur;
     }
-    if (i == K - 1) ranges[2 * cur + 1] = (uint32_t)K;
 }
 
 __global__ __launch_bounds__(kBlock) void k_globalize(const uint32_t *__restrict__ local, int64_t K,
@@ -377,11 +403,11 @@ __global__ __launch_bounds__(kBlock) void k_globalize(const uint32_t *__restrict
 int64_t gsr_scan_blocks(int64_t n) { return (n + kTile - 1) / kTile; }
 
 hipError_t gsr_launch_scan_reduce(const uint32_t *perm, const uint2 *strip_rect, int64_t n,
-                                  uint32_t *partials, hipStream_t s) {
+                                  uint32_t *partials, uint2 *rect_sorted, hipStream_t s) {
     const int64_t nb = gsr_scan_blocks(n);
     if (nb == 0) return hipSuccess;
     hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(kBlock), 0, s, perm, strip_rect, n,
-                       partials);
+                       partials, rect_sorted);
     return hipGetLastError();
 }
 
@@ -391,12 +417,12 @@ hipError_t gsr_launch_scan_partials(uint32_t *partials, int64_t nb, uint64_t *to
     return hipGetLastError();
 }
 
-hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint2 *strip_rect,
+hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint2 *rect_sorted,
                                 const uint32_t *partials, int64_t n, const uint64_t *total,
                                 uint4 *bin, uint32_t *chunk_first, hipStream_t s) {
     const int64_t nb = gsr_scan_blocks(n);
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_scan_down, dim3((unsigned)nb), dim3(kBlock), 0, s, perm, strip_rect,
+    hipLaunchKernelGGL(k_scan_down, dim3((unsigned)nb), dim3(kBlock), 0, s, perm, rect_sorted,
                        partials, n, total, bin, chunk_first);
     return hipGetLastError();
 }
@@ -418,13 +444,13 @@ int64_t gsr_fused_chunks(int64_t K) { return (K + kFChunk - 1) / kFChunk; }
 hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_first, int64_t K,
                                     uint32_t gx, int shift, int nbits, uint32_t *hist,
                                     uint32_t *digit_total, uint32_t *keys_out, uint32_t *vals_out,
-                                    hipStream_t s) {
+                                    uint2 *ranges_zero, uint32_t n_ranges, hipStream_t s) {
     const int64_t nb = gsr_fused_chunks(K);
     if (nb == 0) return hipSuccess;
     const uint32_t nc = (uint32_t)gsr_duplicate_chunks(K);
     const uint32_t mask = (1u << nbits) - 1u;
     hipLaunchKernelGGL(k_dup_count, dim3((unsigned)nb), dim3(kFW * 64), 0, s, bin, chunk_first,
-                       (uint32_t)K, nc, gx, shift, mask, hist, nb);
+                       (uint32_t)K, nc, gx, shift, mask, hist, nb, ranges_zero, n_ranges);
     hipError_t e = gsr_launch_digit_scan(hist, nb, digit_total, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_dup_scatter, dim3((unsigned)nb), dim3(kFW * 64), 0, s, bin, chunk_first,
@@ -436,8 +462,8 @@ hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_firs
 hipError_t gsr_launch_ranges(const uint32_t *tile_keys, int64_t K, uint32_t *ranges,
                              hipStream_t s) {
     if (K == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ranges, dim3((unsigned)((K + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                       tile_keys, K, ranges);
+    hipLaunchKernelGGL(k_ranges, dim3((unsigned)((K + 4 * kBlock - 1) / (4 * kBlock))),
+                       dim3(kBlock), 0, s, tile_keys, K, ranges);
     return hipGetLastError();
 }
 

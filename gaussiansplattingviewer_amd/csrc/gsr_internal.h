@@ -272,13 +272,14 @@ hipError_t gsr_onesweep_sort(uint32_t **keys, uint32_t **vals, uint32_t **keys_a
 // Binning: offsets scan over depth-sorted strip tile counts, duplicate into (tile, id)
 // pairs, and tile ranges.
 int64_t gsr_scan_blocks(int64_t n);
+// also writes rect_sorted[e] = strip_rect[perm[e]]
 hipError_t gsr_launch_scan_reduce(const uint32_t *perm, const uint2 *strip_rect, int64_t n,
-                                  uint32_t *partials, hipStream_t s);
+                                  uint32_t *partials, uint2 *rect_sorted, hipStream_t s);
 hipError_t gsr_launch_scan_partials(uint32_t *partials, int64_t nb, uint64_t *total,
                                     hipStream_t s);
 // bin[e] (e = depth rank, only for Gaussians with pairs) = {exclusive pair offset, Gaussian
 // id, x0 | width << 16, strip-local row0}
-hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint2 *strip_rect,
+hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint2 *rect_sorted,
                                 const uint32_t *partials, int64_t n, const uint64_t *total,
                                 uint4 *bin, uint32_t *chunk_first, hipStream_t s);
 int64_t gsr_duplicate_chunks(int64_t K);
@@ -292,7 +293,7 @@ int64_t gsr_fused_chunks(int64_t K);
 hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_first, int64_t K,
                                     uint32_t gx, int shift, int nbits, uint32_t *hist,
                                     uint32_t *digit_total, uint32_t *keys_out, uint32_t *vals_out,
-                                    hipStream_t s);
+                                    uint2 *ranges_zero, uint32_t n_ranges, hipStream_t s);
 hipError_t gsr_launch_ranges(const uint32_t *tile_keys, int64_t K, uint32_t *ranges,
                              hipStream_t s);
 hipError_t gsr_launch_globalize_tiles(const uint32_t *local, int64_t K, uint32_t offset,
