@@ -45,7 +45,7 @@ struct gsr_context {
     int device = 0;
     // per-Gaussian workspace
     DevBuf records, strip_rect, sort_keys, sort_vals, sort_keys_alt, sort_vals_alt, partials,
-        total, hist, digit_total, bin, chunk_first, rect_sorted;
+        total, hist, digit_total, bin, chunk_first, rect_sorted, pair_count;
     // onesweep sort state: [0,1024) depth-sort digit counts, [1024,2048) tile-sort counts,
     // then the ticket word; look-back granules
     DevBuf sort_ctl, status;
@@ -53,7 +53,9 @@ struct gsr_context {
     // per-pair workspace
     DevBuf tile_keys, tile_vals, tile_keys_alt, tile_vals_alt;
     DevBuf ranges_local;
-    uint64_t *h_total = nullptr;  // pinned
+    uint64_t *h_total = nullptr;  // pinned: [K, look-back flag, K from the preprocess]
+    unsigned long long *d_hostK = nullptr;  // device view of h_total + 2
+    hipEvent_t kcount_ready = nullptr;  // the pair counts of this frame are on the host
     // state of the last forward (for gsr_get_binning)
     bool have_forward = false;
     int64_t last_K = 0;
@@ -70,6 +72,7 @@ struct gsr_context {
     int color_blocks = 512;    // grid cap of the overlapped colour pass
     int aux_low_priority = 1;  // second stream at the lowest priority
     bool serial_color = false; // tuning (env GSR_SERIAL_COLOR): join right after the fork
+    bool late_K = false;       // tuning (env GSR_LATE_K): also sync on the scan's total
     bool split_color = true;   // GSR_OPT_SPLIT_COLOR
     // Stage timing: a ring of event sets, one per forward, read back after the timed region.
     bool timing = false;
@@ -132,6 +135,7 @@ int reserve_P(gsr_context *ctx, int64_t P, hipStream_t s) {
     GSR_TRY(grow(ctx, ctx->sort_vals_alt, n * 4, s));
     GSR_TRY(grow(ctx, ctx->partials, (size_t)std::max<int64_t>(gsr_scan_blocks(P), 1) * 4, s));
     GSR_TRY(grow_zeroed(ctx, ctx->total, 16, s));  // [K (u64), look-back error flag (u32)]
+    GSR_TRY(grow(ctx, ctx->pair_count, 8 * (size_t)((n + 255) / 256), s));  // per block
     GSR_TRY(grow(ctx, ctx->hist, (size_t)gsr_radix_hist_words(P) * 4, s));
     GSR_TRY(grow(ctx, ctx->digit_total, 256 * 4, s));
     GSR_TRY(grow(ctx, ctx->bin, n * 16, s));
@@ -195,7 +199,10 @@ int gsr_create(gsr_context **out) {
         delete ctx;
         return fail(GSR_E_HIP, "gsr_create: no HIP device");
     }
-    if (hipHostMalloc(reinterpret_cast<void **>(&ctx->h_total), 2 * sizeof(uint64_t)) != hipSuccess) {
+    if (hipHostMalloc(reinterpret_cast<void **>(&ctx->h_total), 4 * sizeof(uint64_t),
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->d_hostK), ctx->h_total + 2, 0) !=
+            hipSuccess) {
         (void)hipGetLastError();
         delete ctx;
         return fail(GSR_E_HIP, "gsr_create: hipHostMalloc failed");
@@ -210,10 +217,12 @@ int gsr_create(gsr_context **out) {
     const char *env_cb = std::getenv("GSR_COLOR_BLOCKS");    // tuning: grid cap, 0 = none
     if (env_cb) ctx->color_blocks = std::atoi(env_cb);
     ctx->serial_color = std::getenv("GSR_SERIAL_COLOR") != nullptr;
+    ctx->late_K = std::getenv("GSR_LATE_K") != nullptr;
     bool ok = hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking,
                                           ctx->aux_low_priority ? prio_least : 0) == hipSuccess &&
               hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming) == hipSuccess;
+              hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&ctx->kcount_ready, hipEventDisableTiming) == hipSuccess;
     for (auto &set : ctx->ev)
         for (auto &e : set) ok = ok && hipEventCreate(&e) == hipSuccess;
     for (auto &set : ctx->ev_color)
@@ -241,7 +250,7 @@ void gsr_destroy(gsr_context *ctx) {
                       &ctx->sort_vals,     &ctx->sort_keys_alt, &ctx->sort_vals_alt,
                       &ctx->partials,      &ctx->total,         &ctx->hist,
                       &ctx->digit_total,   &ctx->bin,           &ctx->chunk_first,
-                      &ctx->rect_sorted,
+                      &ctx->rect_sorted,   &ctx->pair_count,
                       &ctx->sort_ctl,      &ctx->status,
                       &ctx->tile_keys,     &ctx->tile_vals,
                       &ctx->tile_keys_alt, &ctx->tile_vals_alt, &ctx->ranges_local};
@@ -255,6 +264,7 @@ void gsr_destroy(gsr_context *ctx) {
             if (e) (void)hipEventDestroy(e);
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
     if (ctx->join) (void)hipEventDestroy(ctx->join);
+    if (ctx->kcount_ready) (void)hipEventDestroy(ctx->kcount_ready);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->h_total) (void)hipHostFree(ctx->h_total);
     if (ctx->blend_stamps) {
@@ -470,6 +480,8 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     pa.sort_keys = static_cast<uint32_t *>(ctx->sort_keys.p);
     pa.sort_vals = static_cast<uint32_t *>(ctx->sort_vals.p);
     pa.strip_rect = static_cast<uint2 *>(ctx->strip_rect.p);
+    pa.block_pairs = static_cast<uint64_t *>(ctx->pair_count.p);
+    pa.host_K = ctx->d_hostK;
     pa.depths = out->depths;
     pa.means2D = out->means2D;
     pa.conic_opacity = out->conic_opacity;
@@ -494,6 +506,10 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         GSR_HIP(hipStreamWaitEvent(ctx->aux, ctx->fork, 0), "hipStreamWaitEvent(fork)");
         if (ctx->timing) GSR_HIP(hipEventRecord(evc[0], ctx->aux), "hipEventRecord");
         GSR_HIP(gsr_launch_color(pa, ctx->color_blocks, ctx->aux), "color launch");
+        // K (the pair count) is on the host once the colour pass ends (k_publish_K stores it
+        // into pinned memory); the host waits for it only after the depth sort and the scan
+        // are enqueued, so the GPU does not idle on the host round trip
+        GSR_HIP(hipEventRecord(ctx->kcount_ready, ctx->aux), "hipEventRecord(pair count)");
         if (ctx->timing) GSR_HIP(hipEventRecord(evc[1], ctx->aux), "hipEventRecord");
         GSR_HIP(hipEventRecord(ctx->join, ctx->aux), "hipEventRecord(join)");
         // every exit from here on (errors included) leaves the caller's stream behind the
@@ -535,13 +551,26 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     GSR_HIP(gsr_launch_scan_reduce(perm, pa.strip_rect, P, partials, rect_sorted, s),
             "scan launch");
     GSR_HIP(gsr_launch_scan_partials(partials, gsr_scan_blocks(P), d_total, s), "scan launch");
-    GSR_HIP(hipMemcpyAsync(ctx->h_total, d_total, 16, hipMemcpyDeviceToHost, s),
-            "hipMemcpyAsync(num_rendered)");
+    const bool check_device_total = ctx->onesweep || dbg || ctx->late_K || !split_color;
+    if (check_device_total)  // onesweep's look-back flag (and, in debug mode, K) from the device
+        GSR_HIP(hipMemcpyAsync(ctx->h_total, d_total, 16, hipMemcpyDeviceToHost, s),
+                "hipMemcpyAsync(num_rendered)");
     GSR_TRY(stage_end(2));
-    GSR_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(num_rendered)");
-    const uint64_t K = ctx->h_total[0];
-    if (ctx->h_total[1] != 0)
-        return fail(GSR_E_HIP, "gsr_forward: radix sort look-back gave up (device flag set)");
+    uint64_t K = 0;
+    if (split_color) {
+        GSR_HIP(hipEventSynchronize(ctx->kcount_ready), "hipEventSynchronize(pair count)");
+        K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
+    }
+    if (check_device_total) {
+        GSR_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(num_rendered)");
+        if (!split_color) K = ctx->h_total[0];
+        if (ctx->h_total[1] != 0)
+            return fail(GSR_E_HIP, "gsr_forward: radix sort look-back gave up (device flag set)");
+        if (ctx->h_total[0] != K)
+            return fail(GSR_E_HIP, "gsr_forward: pair count mismatch (preprocess " +
+                                       std::to_string(K) + ", scan " +
+                                       std::to_string(ctx->h_total[0]) + ")");
+    }
     if (K > (uint64_t)UINT32_MAX - 4096)
         return fail(GSR_E_INVALID, "gsr_forward: more than 2^32-4097 (Gaussian, tile) pairs");
     GSR_TRY(reserve_K(ctx, (int64_t)K, s));

@@ -131,11 +131,10 @@ __device__ __forceinline__ float3 cull_data(float A, float B, float C, float o) 
     return make_float3((float)ex, (float)ey, __uint_as_float(__float_as_uint((float)Lm) + 1u));
 }
 
-// kColor: also evaluate the colour here (one kernel, no second stream).
+// kColor: also evaluate the colour here (one kernel, no second stream).  Returns the number
+// of (Gaussian, strip tile) pairs of Gaussian idx.
 template <bool kColor>
-__global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.P) return;
+__device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, int64_t idx) {
     int32_t radius_out = 0;
     uint32_t strip_tiles = 0, all_tiles = 0;
     uint2 strip_rect = make_uint2(0u, 0u);
@@ -223,6 +222,34 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
     a.sort_keys[idx] = key;
     a.sort_vals[idx] = (uint32_t)idx;
     if (a.tiles_touched) a.tiles_touched[idx] = strip_tiles;
+    return strip_tiles;
+}
+
+// One thread per Gaussian.
+template <bool kColor>
+__global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx < a.P) preprocess_one<kColor>(a, idx);
+}
+
+// One block, after k_color on the second stream (the kernel boundary makes its stores
+// visible): K = sum of k_color's per-block pair counts, stored straight into pinned host
+// memory (system scope) so the host can read it as soon as this kernel's completion event
+// fires -- no copy, and nothing added to the main stream.
+__global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__restrict__ cnt,
+                                                    int64_t n, unsigned long long *host_K) {
+    __shared__ unsigned long long s_w[16];
+    unsigned long long v = 0;
+    for (int64_t i = threadIdx.x; i < n; i += 1024) v += cnt[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int i = 0; i < 16; ++i) t += s_w[i];
+        __hip_atomic_store(host_K, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // Colour of the Gaussians k_preprocess kept (radii > 0, as upstream computes colour only for
@@ -262,11 +289,17 @@ __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t n_waves = (a.P + 63) / 64;
     const int64_t wave_stride = (int64_t)gridDim.x * 4;
+    // K for the host: this thread's (Gaussian, strip tile) pairs (invisible ones have none)
+    unsigned long long pairs = 0;
     for (int64_t wv = (int64_t)blockIdx.x * 4 + w; wv < n_waves; wv += wave_stride) {
         const int64_t base = wv * 64, idx = base + lane;
         const bool in = idx < a.P;
         const bool vis = in && a.radii[idx] != 0;
         if (__ballot(vis) == 0ull) continue;
+        if (vis) {
+            const uint2 r = a.strip_rect[idx];
+            pairs += (unsigned long long)((r.x >> 16) * (r.y >> 16));
+        }
         if (!a.sh_vec4 || a.colors_precomp || a.D != 3) {
             if (vis) color_one(a, idx);
             continue;
@@ -304,6 +337,12 @@ __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
         }
         // the next iteration's LDS writes follow this wave's reads in order
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pairs += __shfl_xor(pairs, o);
+    __shared__ unsigned long long s_w[4];
+    if (lane == 0) s_w[w] = pairs;
+    __syncthreads();
+    if (threadIdx.x == 0) a.block_pairs[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
 }
 
 // GaussianRasterizer.markVisible -> upstream markVisible kernel: in_frustum only.
@@ -349,14 +388,18 @@ hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, bool with_color, hi
         hipLaunchKernelGGL(k_preprocess<true>, dim3(grid_for(a.P)), dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL(k_preprocess<false>, dim3(grid_for(a.P)), dim3(256), 0, s, a);
+
     return hipGetLastError();
 }
 
 hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, hipStream_t s) {
     if (a.P == 0) return hipSuccess;
-    const unsigned g = grid_for(a.P);  // 4 waves of 64 Gaussians per block
-    hipLaunchKernelGGL(k_color, dim3(max_blocks > 0 && (unsigned)max_blocks < g ? max_blocks : g),
-                       dim3(256), 0, s, a);
+    const unsigned g0 = grid_for(a.P);  // 4 waves of 64 Gaussians per block
+    const unsigned g = max_blocks > 0 && (unsigned)max_blocks < g0 ? max_blocks : g0;
+    hipLaunchKernelGGL(k_color, dim3(g), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_publish_K, dim3(1), dim3(1024), 0, s,
+                       reinterpret_cast<const unsigned long long *>(a.block_pairs), (int64_t)g,
+                       a.host_K);
     return hipGetLastError();
 }
 
