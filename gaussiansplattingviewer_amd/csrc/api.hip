@@ -75,7 +75,8 @@ struct gsr_context {
     bool late_K = false;       // tuning (env GSR_LATE_K): also sync on the scan's total
     bool split_color = true;   // GSR_OPT_SPLIT_COLOR
     // Stage timing: a ring of event sets, one per forward, read back after the timed region.
-    bool timing = false;
+    int timing = 0;  // 0 off, 1 every stage, 2 the blend only, on every 8th forward
+    int64_t forwards = 0;  // forwards since gsr_set_timing (mode 2's sampling)
     int64_t timed_frames = 0;
     hipEvent_t ev[kTimingRing][kStages + 1] = {};
     hipEvent_t ev_color[kTimingRing][2] = {};
@@ -220,13 +221,17 @@ int gsr_create(gsr_context **out) {
     ctx->late_K = std::getenv("GSR_LATE_K") != nullptr;
     bool ok = hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking,
                                           ctx->aux_low_priority ? prio_least : 0) == hipSuccess &&
-              hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming) == hipSuccess &&
+              // stream-to-stream hand-offs on one device: a device-scope release suffices
+              hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming | hipEventReleaseToDevice) ==
+                  hipSuccess &&
+              hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming | hipEventReleaseToDevice) ==
+                  hipSuccess &&
               hipEventCreateWithFlags(&ctx->kcount_ready, hipEventDisableTiming) == hipSuccess;
+    // timing events only time: no system-scope fence (cache writeback) when they complete
     for (auto &set : ctx->ev)
-        for (auto &e : set) ok = ok && hipEventCreate(&e) == hipSuccess;
+        for (auto &e : set) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableSystemFence) == hipSuccess;
     for (auto &set : ctx->ev_color)
-        for (auto &e : set) ok = ok && hipEventCreate(&e) == hipSuccess;
+        for (auto &e : set) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableSystemFence) == hipSuccess;
     if (!ok) {
         (void)hipGetLastError();
         gsr_destroy(ctx);
@@ -332,7 +337,9 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
 
 int gsr_set_timing(gsr_context *ctx, int enable) {
     if (!ctx) return fail(GSR_E_INVALID, "gsr_set_timing: NULL context");
-    ctx->timing = enable != 0;
+    if (enable < 0 || enable > 2) return fail(GSR_E_INVALID, "gsr_set_timing: mode 0..2");
+    ctx->timing = enable;
+    ctx->forwards = 0;
     ctx->timed_frames = 0;
     return GSR_OK;
 }
@@ -346,26 +353,24 @@ int gsr_stage_times(gsr_context *ctx, float *ms, int n) {
     const int64_t frames = std::min<int64_t>(ctx->timed_frames, kTimingRing);
     const int64_t last = (ctx->timed_frames - 1) % kTimingRing;
     GSR_HIP(hipEventSynchronize(ctx->ev[last][kStages]), "hipEventSynchronize");
-    double acc[kStages] = {};
+    const bool all = ctx->timing != 2;  // mode 2 recorded the blend's two events only
+    double acc[kAllStages] = {};
     for (int64_t f = 0; f < frames; ++f) {
         const int64_t slot = (ctx->timed_frames - 1 - f) % kTimingRing;
-        for (int i = 0; i < kStages; ++i) {
+        for (int i = all ? 0 : kStages - 1; i < kStages; ++i) {
             float t = 0.f;
             GSR_HIP(hipEventElapsedTime(&t, ctx->ev[slot][i], ctx->ev[slot][i + 1]),
                     "hipEventElapsedTime");
             acc[i] += t;
         }
+        if (all) {
+            float t = 0.f;
+            GSR_HIP(hipEventElapsedTime(&t, ctx->ev_color[slot][0], ctx->ev_color[slot][1]),
+                    "hipEventElapsedTime");
+            acc[kStages] += t;
+        }
     }
-    double acc_color = 0.0;
-    for (int64_t f = 0; f < frames; ++f) {
-        const int64_t slot = (ctx->timed_frames - 1 - f) % kTimingRing;
-        float t = 0.f;
-        GSR_HIP(hipEventElapsedTime(&t, ctx->ev_color[slot][0], ctx->ev_color[slot][1]),
-                "hipEventElapsedTime");
-        acc_color += t;
-    }
-    for (int i = 0; i < kStages && i < n; ++i) ms[i] = (float)(acc[i] / (double)frames);
-    if (n > kStages) ms[kStages] = (float)(acc_color / (double)frames);
+    for (int i = 0; i < kAllStages && i < n; ++i) ms[i] = (float)(acc[i] / (double)frames);
     return kAllStages;
 }
 
@@ -418,8 +423,11 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     ctx->have_forward = false;
     const bool dbg = st->debug != 0;
     hipEvent_t *ev = ctx->ev[ctx->timed_frames % kTimingRing];
+    // this forward's timing: mode 1 every stage; mode 2 the blend, on every 8th forward
+    const int tmode = ctx->timing == 1 ? 1 : (ctx->timing == 2 && ctx->forwards++ % 8 == 0) ? 2 : 0;
     auto stage_end = [&](int i) -> int {
-        if (ctx->timing) GSR_HIP(hipEventRecord(ev[i + 1], s), "hipEventRecord");
+        if (tmode == 1 || (tmode == 2 && i >= 5))
+            GSR_HIP(hipEventRecord(ev[i + 1], s), "hipEventRecord");
         if (dbg) {
             GSR_HIP(hipStreamSynchronize(s), std::string("stage ") + kStageNames[i]);
             GSR_HIP(hipGetLastError(), std::string("stage ") + kStageNames[i]);
@@ -443,7 +451,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         return GSR_OK;
     }
 
-    if (ctx->timing) GSR_HIP(hipEventRecord(ev[0], s), "hipEventRecord");
+    if (tmode == 1) GSR_HIP(hipEventRecord(ev[0], s), "hipEventRecord");
 
     // ---- 1. preprocess -------------------------------------------------------------------
     GsrPreprocessArgs pa{};
@@ -504,20 +512,21 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         // fork: colour on the second stream, overlapped with the depth sort and the binning
         GSR_HIP(hipEventRecord(ctx->fork, s), "hipEventRecord(fork)");
         GSR_HIP(hipStreamWaitEvent(ctx->aux, ctx->fork, 0), "hipStreamWaitEvent(fork)");
-        if (ctx->timing) GSR_HIP(hipEventRecord(evc[0], ctx->aux), "hipEventRecord");
-        GSR_HIP(gsr_launch_color(pa, ctx->color_blocks, ctx->aux), "color launch");
-        // K (the pair count) is on the host once the colour pass ends (k_publish_K stores it
-        // into pinned memory); the host waits for it only after the depth sort and the scan
-        // are enqueued, so the GPU does not idle on the host round trip
+        // K (the pair count) first: k_count_pairs + k_publish_K store it into pinned memory;
+        // the host waits for it only after the depth sort and the scan are enqueued, so the
+        // GPU does not idle on the host round trip
+        GSR_HIP(gsr_launch_count_pairs(pa, ctx->aux), "pair count launch");
         GSR_HIP(hipEventRecord(ctx->kcount_ready, ctx->aux), "hipEventRecord(pair count)");
-        if (ctx->timing) GSR_HIP(hipEventRecord(evc[1], ctx->aux), "hipEventRecord");
+        if (tmode == 1) GSR_HIP(hipEventRecord(evc[0], ctx->aux), "hipEventRecord");
+        GSR_HIP(gsr_launch_color(pa, ctx->color_blocks, ctx->aux), "color launch");
+        if (tmode == 1) GSR_HIP(hipEventRecord(evc[1], ctx->aux), "hipEventRecord");
         GSR_HIP(hipEventRecord(ctx->join, ctx->aux), "hipEventRecord(join)");
         // every exit from here on (errors included) leaves the caller's stream behind the
         // join, so k_color never outlives the caller's view of its inputs
         join_guard.done = false;
         if (dbg) GSR_HIP(hipStreamSynchronize(ctx->aux), "stage color");
         if (ctx->serial_color) GSR_HIP(hipStreamWaitEvent(s, ctx->join, 0), "hipStreamWaitEvent");
-    } else if (ctx->timing) {  // no colour stage: record an empty interval
+    } else if (tmode == 1) {  // no colour stage: record an empty interval
         GSR_HIP(hipEventRecord(evc[0], s), "hipEventRecord");
         GSR_HIP(hipEventRecord(evc[1], s), "hipEventRecord");
     }
@@ -628,6 +637,10 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         GSR_HIP(hipMemsetAsync(ctx->ranges_local.p, 0, T_strip * 8, s), "hipMemsetAsync(ranges)");
     GSR_HIP(gsr_launch_ranges(tk, (int64_t)K, static_cast<uint32_t *>(ctx->ranges_local.p), s),
             "ranges launch");
+    if (!join_guard.done) {  // the blend reads the colours: join the second stream here
+        join_guard.done = true;
+        GSR_HIP(hipStreamWaitEvent(s, ctx->join, 0), "hipStreamWaitEvent(join)");
+    }
     GSR_TRY(stage_end(5));
 
     // ---- 7. blend ------------------------------------------------------------------------------
@@ -650,10 +663,6 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     ba.fast = ctx->fast;
     ba.wave_quadrants = ctx->blend_wave_quadrants;
     ba.stamps = ctx->blend_stamps;
-    if (!join_guard.done) {
-        join_guard.done = true;
-        GSR_HIP(hipStreamWaitEvent(s, ctx->join, 0), "hipStreamWaitEvent(join)");
-    }
     GSR_HIP(gsr_launch_blend(ba, s), "blend launch");
     GSR_TRY(stage_end(6));
 
@@ -664,7 +673,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     ctx->last_tiles_local = tk;
 
     ctx->have_forward = true;
-    if (ctx->timing) ++ctx->timed_frames;
+    if (tmode) ++ctx->timed_frames;
     return GSR_OK;
 }
 

@@ -213,7 +213,7 @@ struct GsrPreprocessArgs {
     // per Gaussian: strip-clipped tile rect {x0 | width << 16, strip-local row0 | rows << 16},
     // {0, 0} when it has no pair in the strip (grid dimensions < 2^16, checked by the host)
     uint2 *strip_rect;
-    uint64_t *block_pairs;  // per k_color block: its (Gaussian, strip tile) pair count
+    uint64_t *block_pairs;  // per k_count_pairs block: its (Gaussian, strip tile) pair count
     unsigned long long *host_K;  // pinned host memory (device-mapped): K of this frame
     // optional debug outputs
     float *depths, *means2D, *conic_opacity, *rgb;
@@ -223,9 +223,10 @@ struct GsrPreprocessArgs {
 // with_color: evaluate the colour in the same kernel (else gsr_launch_color does it).
 hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, bool with_color, hipStream_t s);
 // SH -> RGB (or colors_precomp) of every Gaussian with radii > 0 into SplatRecord.c.yzw (+ rgb)
-// max_blocks > 0 caps the grid (grid-stride loop).  Also counts the frame's pairs and
-// launches k_publish_K: K -> *a.host_K (pinned host memory), after the colour kernel.
+// max_blocks > 0 caps the grid (grid-stride loop).
 hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, hipStream_t s);
+// K of the frame (sum of the strip rects' pair counts) -> *a.host_K (pinned host memory).
+hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s);
 hipError_t gsr_launch_mark_visible(const float *means3D, int64_t P, const float *viewmatrix,
                                    uint8_t *visible, hipStream_t s);
 hipError_t gsr_launch_view_depth_keys(const float *xyz, int64_t P, float v20, float v21, float v22,

@@ -11,6 +11,8 @@
 //    the record's colour.  It depends only on k_preprocess's radii and nothing before the
 //    blend reads colour, so api.hip runs it on a second stream, overlapped with the depth
 //    sort and the binning (which are latency-bound and leave most CUs idle).
+#include <algorithm>
+
 #include "gsr_internal.h"
 
 using namespace gsr;
@@ -232,10 +234,10 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
     if (idx < a.P) preprocess_one<kColor>(a, idx);
 }
 
-// One block, after k_color on the second stream (the kernel boundary makes its stores
-// visible): K = sum of k_color's per-block pair counts, stored straight into pinned host
-// memory (system scope) so the host can read it as soon as this kernel's completion event
-// fires -- no copy, and nothing added to the main stream.
+// One block, after k_count_pairs on the second stream (the kernel boundary makes its stores
+// visible): K = sum of the per-block pair counts, stored straight into pinned host memory
+// (system scope) so the host can read it as soon as this kernel's completion event fires --
+// no copy, and nothing added to the main stream.
 __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__restrict__ cnt,
                                                     int64_t n, unsigned long long *host_K) {
     __shared__ unsigned long long s_w[16];
@@ -289,17 +291,11 @@ __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t n_waves = (a.P + 63) / 64;
     const int64_t wave_stride = (int64_t)gridDim.x * 4;
-    // K for the host: this thread's (Gaussian, strip tile) pairs (invisible ones have none)
-    unsigned long long pairs = 0;
     for (int64_t wv = (int64_t)blockIdx.x * 4 + w; wv < n_waves; wv += wave_stride) {
         const int64_t base = wv * 64, idx = base + lane;
         const bool in = idx < a.P;
         const bool vis = in && a.radii[idx] != 0;
         if (__ballot(vis) == 0ull) continue;
-        if (vis) {
-            const uint2 r = a.strip_rect[idx];
-            pairs += (unsigned long long)((r.x >> 16) * (r.y >> 16));
-        }
         if (!a.sh_vec4 || a.colors_precomp || a.D != 3) {
             if (vis) color_one(a, idx);
             continue;
@@ -337,12 +333,25 @@ __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
         }
         // the next iteration's LDS writes follow this wave's reads in order
     }
+}
+
+// K for the host, on the second stream right after the preprocess: per-block sums of the
+// (Gaussian, strip tile) pair counts from the packed strip rects (grid-stride, 256 blocks).
+constexpr int kCountBlocks = 256;
+__global__ __launch_bounds__(256) void k_count_pairs(const uint2 *__restrict__ strip_rect,
+                                                     int64_t P,
+                                                     unsigned long long *__restrict__ block_pairs) {
+    unsigned long long v = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P; i += (int64_t)gridDim.x * 256) {
+        const uint2 r = strip_rect[i];
+        v += (unsigned long long)((r.x >> 16) * (r.y >> 16));
+    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) pairs += __shfl_xor(pairs, o);
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     __shared__ unsigned long long s_w[4];
-    if (lane == 0) s_w[w] = pairs;
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
     __syncthreads();
-    if (threadIdx.x == 0) a.block_pairs[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    if (threadIdx.x == 0) block_pairs[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
 }
 
 // GaussianRasterizer.markVisible -> upstream markVisible kernel: in_frustum only.
@@ -397,6 +406,14 @@ hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, hipStrea
     const unsigned g0 = grid_for(a.P);  // 4 waves of 64 Gaussians per block
     const unsigned g = max_blocks > 0 && (unsigned)max_blocks < g0 ? max_blocks : g0;
     hipLaunchKernelGGL(k_color, dim3(g), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s) {
+    if (a.P == 0) return hipSuccess;
+    const unsigned g = std::min<unsigned>(kCountBlocks, grid_for(a.P));
+    hipLaunchKernelGGL(k_count_pairs, dim3(g), dim3(256), 0, s, a.strip_rect, a.P,
+                       reinterpret_cast<unsigned long long *>(a.block_pairs));
     hipLaunchKernelGGL(k_publish_K, dim3(1), dim3(1024), 0, s,
                        reinterpret_cast<const unsigned long long *>(a.block_pairs), (int64_t)g,
                        a.host_K);

@@ -130,7 +130,9 @@ int gsr_depth_argsort(gsr_context *ctx, const float *xyz, int64_t P, const float
  * gsr_set_timing(1) starts recording one event set per forward (a ring of the last 256);
  * gsr_stage_times waits for the last timed forward and writes the MEAN per-stage time (ms)
  * over the recorded forwards into ms[i] for i < n; it returns the number of stages.
- * Stage names via gsr_stage_name(i). */
+ * Stage names via gsr_stage_name(i).  Each event costs the stream a few microseconds, so
+ * gsr_set_timing(2) records only the two events around the blend (the other stages read 0).
+ * gsr_set_timing(0) stops recording. */
 int gsr_set_timing(gsr_context *ctx, int enable);
 int gsr_stage_times(gsr_context *ctx, float *ms, int n);
 const char *gsr_stage_name(int i);
