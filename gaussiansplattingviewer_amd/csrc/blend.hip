@@ -74,6 +74,7 @@ constexpr int kBatch = 256;  // splats staged in LDS per round
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 
+
 // One staged splat as the inner loop reads it: three 16-B LDS reads from one address.
 struct StagedSplat {
     float4 g;  // x, y, conic a, conic b      (fast: prescaled a, b)
@@ -122,14 +123,17 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
                 __builtin_fmaf(dx, __builtin_fmaf(sp.g.z, dx, sp.g.w * dy), sp.q.x * dy * dy);
             const float alpha = fminf(0.99f, sp.q.y * __builtin_amdgcn_exp2f(p2));
             vis = !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
-            const float aT = alpha * T;
-            test_T = T - aT;  // T (1 - alpha), rounded differently
-            acc = vis && !(test_T < 0.0001f);
-            term = vis && (test_T < 0.0001f);
-            wgt = acc ? aT : 0.0f;
+            // same arithmetic as k_blend_q (short loop-carried chain through T)
+            const float om = vis ? 1.0f - alpha : 1.0f;
+            test_T = T * om;
+            const bool lo = test_T < 0.0001f;
+            wgt = lo ? 0.0f : T - test_T;
             C0 = __builtin_fmaf(sp.q.z, wgt, C0);
             C1 = __builtin_fmaf(sp.q.w, wgt, C1);
             C2 = __builtin_fmaf(sp.e.x, wgt, C2);
+            last_contributor = (vis && !lo) ? __float_as_uint(sp.e.y) : last_contributor;
+            T = lo ? -fabsf(T) : test_T;
+            return;
         } else {
             // upstream renderCUDA per-pixel body, same operation order
             const float power =
@@ -259,15 +263,23 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
     }
 }
 
+// Block -> work item, XCD-aware: the hardware dispatches block b to XCD b % 8; groups of
+// `group` consecutive work items (a tile's quadrants and its row neighbours) go round-robin
+// over the XCDs, so each group shares one L2 while the image's heavy and light regions are
+// spread evenly over the 8 XCDs.  group = 0: plain order.
+__device__ __forceinline__ uint32_t xcd_work(uint32_t b, uint32_t group) {
+    if (group == 0) return b;
+    const uint32_t x = b & 7u, l = b >> 3;
+    return ((l / group) * 8u + x) * group + l % group;
+}
+
 // One wave per (tile, 8x8 quadrant), 64-thread blocks, no block barriers: each wave streams
 // its tile's list 64 splats at a time, culls them against its own quadrant, compacts the
 // survivors and composites them, and stops as soon as its own 64 pixels are done -- so a
 // quadrant never waits for the slowest quadrant of its tile (the 4-wave kernel's batch
 // barriers cost ~40 % of wave time, measured with GSR_DEBUG_BLEND_STAMPS).  Record gathers
 // are software-pipelined: a chunk's records are loaded while the previous chunk is
-// composited, their ids one chunk earlier still.  Blocks are mapped XCD-aware: hardware
-// dispatches block b to XCD b % 8, so work item (b % 8) * per_xcd + b / 8 keeps the four
-// quadrants of a tile (and neighbouring tiles) on one XCD's L2.
+// composited, their ids one chunk earlier still.  Blocks are mapped XCD-aware (xcd_work).
 template <bool kFast>
 __global__ __launch_bounds__(64) void k_blend_q(const GsrBlendArgs a, uint32_t n_work,
                                                 uint32_t per_xcd) {
@@ -275,7 +287,7 @@ __global__ __launch_bounds__(64) void k_blend_q(const GsrBlendArgs a, uint32_t n
     __shared__ uint16_t s_list[64 + 2];
 
     const uint32_t b = blockIdx.x;
-    const uint32_t work = (b & 7u) * per_xcd + (b >> 3);
+    const uint32_t work = xcd_work(b, a.xcd_group);
     if (work >= n_work) return;
     const int lane = threadIdx.x;
     const uint32_t tile = work >> 2, quad = work & 3u;
@@ -303,18 +315,23 @@ __global__ __launch_bounds__(64) void k_blend_q(const GsrBlendArgs a, uint32_t n
         bool vis, acc, term;
         float test_T;
         if (kFast) {
+            // The loop-carried chain is only T -> T (1 - alpha_eff) -> compare -> select:
+            // alpha_eff = 0 for an invisible splat (then test_T = T and the weight T - test_T
+            // is 0), and a pixel that terminates keeps -|T| (idempotent once done).
             const float p2 =
                 __builtin_fmaf(dx, __builtin_fmaf(sp.g.z, dx, sp.g.w * dy), sp.q.x * dy * dy);
             const float alpha = fminf(0.99f, sp.q.y * __builtin_amdgcn_exp2f(p2));
             vis = !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
-            const float aT = alpha * T;
-            test_T = T - aT;
-            acc = vis && !(test_T < 0.0001f);
-            term = vis && (test_T < 0.0001f);
-            const float wgt = acc ? aT : 0.0f;
+            const float om = vis ? 1.0f - alpha : 1.0f;
+            test_T = T * om;
+            const bool lo = test_T < 0.0001f;
+            const float wgt = lo ? 0.0f : T - test_T;
             C0 = __builtin_fmaf(sp.q.z, wgt, C0);
             C1 = __builtin_fmaf(sp.q.w, wgt, C1);
             C2 = __builtin_fmaf(sp.e.x, wgt, C2);
+            last_contributor = (vis && !lo) ? __float_as_uint(sp.e.y) : last_contributor;
+            T = lo ? -fabsf(T) : test_T;
+            return;
         } else {
             const float power =
                 -0.5f * (sp.g.z * dx * dx + sp.q.x * dy * dy) - sp.g.w * dx * dy;
@@ -409,11 +426,151 @@ __global__ __launch_bounds__(64) void k_blend_q(const GsrBlendArgs a, uint32_t n
     }
 }
 
+// Fast arithmetic, packed, one wave per (tile, 16x8 half): like k_blend_q, but each lane
+// owns the two pixels (x, y) and (x + 8, y), so the per-pixel math runs as v_pk_* float2
+// instructions (2 pixels per instruction where CDNA4 has packed f32 ops), and the splat-side
+// work (LDS reads, list handling, loop control) is shared by two pixels.  A splat is kept if
+// it may touch the 16x8 half (one cull test on the half's box).
+__global__ __launch_bounds__(64) void k_blend_h(const GsrBlendArgs a, uint32_t n_work,
+                                                uint32_t per_xcd) {
+    __shared__ StagedSplat s_spl[64 + 1];  // slot 64: opacity-0 pad
+    __shared__ uint16_t s_list[64 + 2];
+
+    const uint32_t b = blockIdx.x;
+    const uint32_t work = xcd_work(b, a.xcd_group);
+    if (work >= n_work) return;
+    const int lane = threadIdx.x;
+    const uint32_t tile = work >> 1, half = work & 1u;
+    const uint32_t tx = tile % a.grid_x, ty_local = tile / a.grid_x, ty = a.row_begin + ty_local;
+    const int hx0 = (int)tx * GSR_TILE_X, hy0 = (int)ty * GSR_TILE_Y + (int)half * 8;
+    const int pxa = hx0 + (lane & 7), pxb = pxa + 8, py = hy0 + (lane >> 3);
+    const bool in_a = pxa < a.W && py < a.H, in_b = pxb < a.W && py < a.H;
+    const v2f pfx = {(float)pxa, (float)pxb};
+    const float pfy = (float)py;
+    if (lane == 0) {
+        s_spl[64].g = make_float4(0.f, 0.f, 0.f, 0.f);
+        s_spl[64].q = make_float4(0.f, 0.f, 0.f, 0.f);
+        s_spl[64].e = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+
+    const uint2 range = a.ranges[tile];
+    v2f T = {in_a ? 1.0f : -1.0f, in_b ? 1.0f : -1.0f};  // done in the sign, as k_blend
+    v2f C0 = {0.0f, 0.0f}, C1 = {0.0f, 0.0f}, C2 = {0.0f, 0.0f};
+    uint32_t last_a = 0, last_b = 0;
+    auto live_any = [&]() { return __ballot(!(T.x <= 0.0f) || !(T.y <= 0.0f)) != 0ull; };
+    if (!live_any()) return;
+
+    auto composite = [&](const StagedSplat &sp) {
+        const v2f dx = (v2f)sp.g.x - pfx;
+        const float dy = sp.g.y - pfy;
+        const v2f ady = __builtin_elementwise_fma((v2f)sp.g.z, dx, (v2f)(sp.g.w * dy));
+        const v2f p2 = __builtin_elementwise_fma(dx, ady, (v2f)(sp.q.x * dy * dy));
+        v2f e;
+        e.x = __builtin_amdgcn_exp2f(p2.x);
+        e.y = __builtin_amdgcn_exp2f(p2.y);
+        const v2f oe = (v2f)sp.q.y * e;
+        v2f alpha;
+        alpha.x = fminf(0.99f, oe.x);
+        alpha.y = fminf(0.99f, oe.y);
+        const v2f aT = alpha * T;
+        const v2f test_T = T - aT;
+        const bool vis_a = !(p2.x > 0.0f) && !(alpha.x < 1.0f / 255.0f);
+        const bool vis_b = !(p2.y > 0.0f) && !(alpha.y < 1.0f / 255.0f);
+        const bool lo_a = test_T.x < 0.0001f, lo_b = test_T.y < 0.0001f;
+        const bool acc_a = vis_a && !lo_a, acc_b = vis_b && !lo_b;
+        v2f wgt;
+        wgt.x = acc_a ? aT.x : 0.0f;
+        wgt.y = acc_b ? aT.y : 0.0f;
+        C0 = __builtin_elementwise_fma((v2f)sp.q.z, wgt, C0);
+        C1 = __builtin_elementwise_fma((v2f)sp.q.w, wgt, C1);
+        C2 = __builtin_elementwise_fma((v2f)sp.e.x, wgt, C2);
+        T.x = acc_a ? test_T.x : ((vis_a && lo_a) ? -fabsf(T.x) : T.x);
+        T.y = acc_b ? test_T.y : ((vis_b && lo_b) ? -fabsf(T.y) : T.y);
+        const uint32_t pos = __float_as_uint(sp.e.y);
+        last_a = acc_a ? pos : last_a;
+        last_b = acc_b ? pos : last_b;
+    };
+    const char *lds = reinterpret_cast<const char *>(s_spl);
+    auto fetch = [&](uint32_t off) { return *reinterpret_cast<const StagedSplat *>(lds + off); };
+    const float X0 = (float)hx0, Y0 = (float)hy0;
+    const float kL2e = 1.4426950408889634f;
+
+    uint32_t i0 = range.x + (uint32_t)lane;
+    uint32_t id_next = i0 + 64u < range.y ? a.point_list[i0 + 64u] : 0u;
+    SplatRecord r_next;
+    if (i0 < range.y) r_next = a.records[a.point_list[i0]];
+    for (uint32_t start = range.x; start < range.y; start += 64) {
+        const uint32_t idx = start + (uint32_t)lane;
+        const bool valid = idx < range.y;
+        const SplatRecord r = r_next;
+        if (idx + 64u < range.y) r_next = a.records[id_next];
+        if (idx + 128u < range.y) id_next = a.point_list[idx + 128u];
+
+        bool keep = valid;
+        if (valid && a.cull)
+            keep = may_touch(r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.z, r.b.w, 2.0f * r.c.x, X0,
+                             X0 + 15, Y0, Y0 + 7);
+        const uint64_t bal = __ballot(keep);
+        if (keep) {
+            StagedSplat st;
+            st.g = make_float4(r.a.x, r.a.y, r.a.z * (-0.5f * kL2e), r.a.w * (-kL2e));
+            st.q = make_float4(r.b.x * (-0.5f * kL2e), r.b.y, r.c.y, r.c.z);
+            st.e = make_float4(r.c.w, __uint_as_float(idx - range.x + 1u), 0.0f, 0.0f);
+            const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+            s_spl[__popcll(bal & lt)] = st;
+        }
+        int count = __popcll(bal);
+        if (count == 0) continue;
+        if (lane < count) s_list[lane] = (uint16_t)(lane * sizeof(StagedSplat));
+        if (count & 1) {
+            if (lane == 0) s_list[count] = (uint16_t)(64 * sizeof(StagedSplat));
+            ++count;
+        }
+        auto next2 = [&](int k) { return k + 2 < count ? k + 2 : count - 2; };
+        StagedSplat a0 = fetch(s_list[0]), a1 = fetch(s_list[1]);
+        for (int k = 0;;) {
+            int kn = next2(k);
+            const StagedSplat b0 = fetch(s_list[kn]), b1 = fetch(s_list[kn + 1]);
+            composite(a0);
+            composite(a1);
+            k += 2;
+            if (k >= count) break;
+            kn = next2(k);
+            a0 = fetch(s_list[kn]);
+            a1 = fetch(s_list[kn + 1]);
+            composite(b0);
+            composite(b1);
+            k += 2;
+            if (k >= count) break;
+        }
+        if (!live_any()) break;
+    }
+
+    const int row = py - a.y0;
+    const size_t plane = (size_t)a.rows_out * a.W;
+    const float Ta = fabsf(T.x), Tb = fabsf(T.y);
+    if (in_a) {
+        const size_t pid = (size_t)row * a.W + pxa;
+        if (a.final_T) a.final_T[pid] = Ta;
+        if (a.n_contrib) a.n_contrib[pid] = last_a;
+        a.out_color[pid] = C0.x + Ta * a.bg[0];
+        a.out_color[plane + pid] = C1.x + Ta * a.bg[1];
+        a.out_color[2 * plane + pid] = C2.x + Ta * a.bg[2];
+    }
+    if (in_b) {
+        const size_t pid = (size_t)row * a.W + pxb;
+        if (a.final_T) a.final_T[pid] = Tb;
+        if (a.n_contrib) a.n_contrib[pid] = last_b;
+        a.out_color[pid] = C0.y + Tb * a.bg[0];
+        a.out_color[plane + pid] = C1.y + Tb * a.bg[1];
+        a.out_color[2 * plane + pid] = C2.y + Tb * a.bg[2];
+    }
+}
+
 // Fast arithmetic, packed: a 2-wave block per 16x16 tile; wave w owns rows 8w..8w+7 and each
 // lane owns the two pixels (x, y) and (x + 8, y) of its row, so every per-pixel operation
 // runs as one v_pk_* instruction on a float2 (CDNA4 reaches its fp32 rate only with packed
 // math).  A wave iterates over the splats that touch either of its two 8x8 quadrants.
-typedef float v2f __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(128) void k_blend_fast2(const GsrBlendArgs a) {
     __shared__ StagedSplat s_spl[kBatch + 1];  // slot kBatch: opacity-0 pad (see k_blend)
@@ -562,9 +719,18 @@ __global__ __launch_bounds__(128) void k_blend_fast2(const GsrBlendArgs a) {
 
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s) {
     if (a.rows_tiles == 0 || a.grid_x == 0) return hipSuccess;
-    if (a.wave_quadrants && a.fast != 2) {
+    if (a.wave_quadrants && a.fast == 2) {
+        const uint32_t n_work = 2u * a.grid_x * a.rows_tiles;
+        const uint32_t g = a.xcd_group ? a.xcd_group * 8u : 8u;
+        const uint32_t per_xcd = (n_work + g - 1) / g * g / 8u;
+        hipLaunchKernelGGL(k_blend_h, dim3(8u * per_xcd), dim3(64), 0, s, a, n_work, per_xcd);
+        return hipGetLastError();
+    }
+    if (a.wave_quadrants) {
         const uint32_t n_work = 4u * a.grid_x * a.rows_tiles;
-        const uint32_t per_xcd = (n_work + 7u) / 8u;
+        // grid: whole groups on every XCD (blocks past n_work exit)
+        const uint32_t g = a.xcd_group ? a.xcd_group * 8u : 8u;
+        const uint32_t per_xcd = (n_work + g - 1) / g * g / 8u;
         if (a.fast)
             hipLaunchKernelGGL((k_blend_q<true>), dim3(8u * per_xcd), dim3(64), 0, s, a, n_work,
                                per_xcd);
