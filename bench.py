@@ -33,7 +33,7 @@ from gaussiansplattingviewer_amd import _lib  # noqa: E402
 from gaussiansplattingviewer_amd.camera import cuda_camera_inputs, orbit_eye, static_camera  # noqa: E402
 from gaussiansplattingviewer_amd.gaussian_data import synthetic_gaussians  # noqa: E402
 from gaussiansplattingviewer_amd.rasterizer import rasterize_gaussians_native  # noqa: E402
-from gaussiansplattingviewer_amd.strips import gather_strips, strip_rows  # noqa: E402
+from gaussiansplattingviewer_amd.strips import StripGather, strip_rows  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 
@@ -174,11 +174,22 @@ def main():
     gy = (H + 15) // 16
     rows = strip_rows(gy, world, rank) if world > 1 else None
 
+    # N > 1: each rank renders its strip of tile rows; rank 0 gathers the frame (RCCL).  The
+    # gather of frame i runs asynchronously while frame i+1 renders (at most two frames in
+    # flight); the last frame's gather completes inside the timed region.
+    gather = StripGather(H, W, world, rank, device=dev) if world > 1 else None
+
     def step(i):
         res = scene.render(i, rows)
-        if world > 1:
-            gather_strips(res.color, H, W, world, rank)
+        if gather is not None:
+            if gather.pending:
+                gather.finish()
+            gather.submit(res.color)
         return res
+
+    def drain():
+        while gather is not None and gather.pending:
+            gather.finish()
 
     lib = _lib.load_library()
     ctx = _lib.context(local)
@@ -202,6 +213,7 @@ def main():
     # Warmup (also sizes the workspace so the timed loop never allocates).
     for i in range(args.warmup):
         step(i)
+    drain()
     torch.cuda.synchronize()
 
     # Timed region: HIP events around the dominant kernel (the blend) only -- every event
@@ -217,6 +229,7 @@ def main():
     K_total = 0
     for i in range(args.steps):
         K_total += step(args.warmup + i).num_rendered
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -228,6 +241,7 @@ def main():
     _lib.check(lib.gsr_set_timing(ctx, 1), "gsr_set_timing")
     for i in range(min(args.steps, 30)):
         step(i)
+    drain()
     _lib.check(lib.gsr_stage_times(ctx, buf, len(names)), "gsr_stage_times")
     _lib.check(lib.gsr_set_timing(ctx, 0), "gsr_set_timing")
     stage_ms = {n: float(buf[i]) for i, n in enumerate(names)}

@@ -59,6 +59,54 @@ def gather_strips(strip: torch.Tensor, H: int, W: int, world: int, rank: int,
     return None
 
 
+class StripGather:
+    """Pipelined strip gather for a stream of frames: `submit(strip)` starts the asynchronous
+    gather of one frame's strips to rank 0 (RCCL runs it on its own stream, after the render
+    that produced the strip) and returns at once; `finish()` waits for the oldest submitted
+    frame and returns it on rank 0 (None elsewhere).  Submitting frame i+1 before finishing
+    frame i overlaps the gather with the next render, as a display swap chain would.
+
+    Buffers are allocated once: a padded send strip per in-flight frame and, on rank 0, the
+    (world, 3, hmax, W) receive block; the frame is assembled with one `cat` of the valid rows.
+    """
+
+    def __init__(self, H: int, W: int, world: int, rank: int, dtype=torch.float32,
+                 device=None, group=None, depth: int = 2):
+        gy = (H + 15) // 16
+        self.H, self.W, self.world, self.rank, self.group = H, W, world, rank, group
+        self.layout = [strip_pixel_rows(strip_rows(gy, world, r), H) for r in range(world)]
+        self.hmax = max(rows for _, rows in self.layout)
+        self.rows_me = self.layout[rank][1]
+        self.slots = [{
+            "send": torch.zeros((3, self.hmax, W), dtype=dtype, device=device),
+            "recv": (torch.empty((world, 3, self.hmax, W), dtype=dtype, device=device)
+                     if rank == 0 else None),
+        } for _ in range(depth)]
+        self.next_slot = 0
+        self.pending = []  # (slot, work)
+
+    def submit(self, strip: torch.Tensor) -> None:
+        if strip.shape != (3, self.rows_me, self.W):
+            raise ValueError(f"strip shape {tuple(strip.shape)} != (3, {self.rows_me}, {self.W})")
+        if len(self.pending) == len(self.slots):
+            raise RuntimeError("StripGather: every slot is in flight; call finish() first")
+        slot = self.slots[self.next_slot]
+        self.next_slot = (self.next_slot + 1) % len(self.slots)
+        slot["send"][:, :self.rows_me].copy_(strip)
+        parts = list(slot["recv"].unbind(0)) if self.rank == 0 else None
+        work = dist.gather(slot["send"], parts, dst=0, group=self.group, async_op=True)
+        self.pending.append((slot, work))
+
+    def finish(self) -> torch.Tensor | None:
+        slot, work = self.pending.pop(0)
+        work.wait()
+        if self.rank != 0:
+            return None
+        recv = slot["recv"]
+        return torch.cat([recv[r, :, :rows] for r, (_, rows) in enumerate(self.layout) if rows],
+                         dim=1)
+
+
 def render_strips(render_fn, H: int, W: int, world: int, rank: int, group=None):
     """Render this rank's strip with `render_fn(tile_rows) -> (3, rows, W) tensor` and gather
     the frame on rank 0 (None elsewhere)."""
