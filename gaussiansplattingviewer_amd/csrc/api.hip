@@ -45,7 +45,7 @@ struct gsr_context {
     int device = 0;
     // per-Gaussian workspace
     DevBuf records, strip_rect, sort_keys, sort_vals, sort_keys_alt, sort_vals_alt, partials,
-        total, hist, digit_total, bin, chunk_first, rect_sorted, pair_count;
+        total, hist, digit_total, bin, chunk_first, rect_sorted, pair_count, valid_count;
     // onesweep sort state: [0,1024) depth-sort digit counts, [1024,2048) tile-sort counts,
     // then the ticket word; look-back granules
     DevBuf sort_ctl, status;
@@ -139,7 +139,8 @@ int reserve_P(gsr_context *ctx, int64_t P, hipStream_t s) {
     GSR_TRY(grow_zeroed(ctx, ctx->total, 16, s));  // [K (u64), look-back error flag (u32)]
     GSR_TRY(grow(ctx, ctx->pair_count, 8 * (size_t)((n + 255) / 256), s));  // per block
     GSR_TRY(grow(ctx, ctx->hist, (size_t)gsr_radix_hist_words(P) * 4, s));
-    GSR_TRY(grow(ctx, ctx->digit_total, 256 * 4, s));
+    GSR_TRY(grow(ctx, ctx->digit_total, 256 * 4 * GSR_RADIX_MAX_PASSES, s));  // a slice / pass
+    GSR_TRY(grow(ctx, ctx->valid_count, 4, s));
     GSR_TRY(grow(ctx, ctx->bin, n * 16, s));
     GSR_TRY(grow(ctx, ctx->rect_sorted, n * 8, s));
     GSR_TRY(grow_zeroed(ctx, ctx->sort_ctl, 2048 * 4 + 256, s));
@@ -258,7 +259,7 @@ void gsr_destroy(gsr_context *ctx) {
                       &ctx->sort_vals,     &ctx->sort_keys_alt, &ctx->sort_vals_alt,
                       &ctx->partials,      &ctx->total,         &ctx->hist,
                       &ctx->digit_total,   &ctx->bin,           &ctx->chunk_first,
-                      &ctx->rect_sorted,   &ctx->pair_count,
+                      &ctx->rect_sorted,   &ctx->pair_count,    &ctx->valid_count,
                       &ctx->sort_ctl,      &ctx->status,
                       &ctx->tile_keys,     &ctx->tile_vals,
                       &ctx->tile_keys_alt, &ctx->tile_vals_alt, &ctx->ranges_local};
@@ -541,6 +542,8 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     uint32_t *dv_alt = static_cast<uint32_t *>(ctx->sort_vals_alt.p);
     uint32_t *hist = static_cast<uint32_t *>(ctx->hist.p);
     uint32_t *digit_total = static_cast<uint32_t *>(ctx->digit_total.p);
+    // sorted entries: all P (onesweep) or, compacting, the count the sort stores here
+    uint32_t *d_valid = ctx->onesweep ? nullptr : static_cast<uint32_t *>(ctx->valid_count.p);
     if (ctx->onesweep) {
         GSR_TRY(epoch_guard(ctx, 8, s));
         // zero both digit-count blocks (depth + tile sort) once per frame
@@ -549,8 +552,10 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
                                   onesweep_ws(ctx, 0), s),
                 "depth sort launch");
     } else {
+        // compacting: Gaussians without pairs in the strip (sentinel keys) are dropped by the
+        // first pass; the count of the rest lands in valid_count (device)
         GSR_HIP(gsr_radix_sort_pairs(&dk, &dv, &dk_alt, &dv_alt, P, 0, 32, hist, digit_total, s,
-                                     ctx->depth_sort_shape),
+                                     ctx->depth_sort_shape, 0, d_valid),
                 "depth sort launch");
     }
     GSR_TRY(stage_end(1));
@@ -560,7 +565,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     uint32_t *partials = static_cast<uint32_t *>(ctx->partials.p);
     uint64_t *d_total = static_cast<uint64_t *>(ctx->total.p);
     uint2 *rect_sorted = static_cast<uint2 *>(ctx->rect_sorted.p);
-    GSR_HIP(gsr_launch_scan_reduce(perm, pa.strip_rect, P, partials, rect_sorted, s),
+    GSR_HIP(gsr_launch_scan_reduce(perm, pa.strip_rect, P, d_valid, partials, rect_sorted, s),
             "scan launch");
     GSR_HIP(gsr_launch_scan_partials(partials, gsr_scan_blocks(P), d_total, s), "scan launch");
     const bool check_device_total = ctx->onesweep || dbg || ctx->late_K || !split_color;
@@ -599,8 +604,8 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     const GsrRadixPlan tplan = gsr_radix_plan(0, tbits);
     const bool fused = !ctx->onesweep && ctx->fused_binning;
     if (K > 0) {
-        GSR_HIP(gsr_launch_scan_down(perm, rect_sorted, partials, P, d_total, bin, chunk_first,
-                                     s),
+        GSR_HIP(gsr_launch_scan_down(perm, rect_sorted, partials, P, d_valid, d_total, bin,
+                                     chunk_first, s),
                 "scan_down launch");
         if (fused) {
             // duplicate fused with the first tile-sort pass (a single pass when tbits == 0)

@@ -25,12 +25,19 @@ constexpr uint32_t kChunk = 2048;        // output pairs per duplicate block
 // coalesced instead of gathering them a second time.
 __device__ __forceinline__ uint32_t rect_count(uint2 r) { return (r.x >> 16) * (r.y >> 16); }
 
+// d_n (if set): the depth sort's count of sorted entries (the rest of perm is stale).
 __global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t *__restrict__ perm,
                                                         const uint2 *__restrict__ strip_rect,
-                                                        int64_t n, uint32_t *__restrict__ partials,
+                                                        int64_t n_max, const uint32_t *d_n,
+                                                        uint32_t *__restrict__ partials,
                                                         uint2 *__restrict__ rect_sorted) {
     __shared__ uint32_t s_tmp[4];
+    const int64_t n = d_n ? (int64_t)*d_n : n_max;
     const int64_t base = (int64_t)blockIdx.x * kTile;
+    if (base >= n) {  // whole block: an empty partial
+        if (threadIdx.x == 0) partials[blockIdx.x] = 0;
+        return;
+    }
     uint32_t sum = 0;
 #pragma unroll 4
     for (int j = 0; j < kItems; ++j) {
@@ -72,10 +79,13 @@ __global__ __launch_bounds__(kBlock) void k_scan_partials(uint32_t *__restrict__
 __global__ __launch_bounds__(kBlock) void k_scan_down(const uint32_t *__restrict__ perm,
                                                       const uint2 *__restrict__ rect_sorted,
                                                       const uint32_t *__restrict__ partials,
-                                                      int64_t n, const uint64_t *__restrict__ total,
+                                                      int64_t n_max, const uint32_t *d_n,
+                                                      const uint64_t *__restrict__ total,
                                                       uint4 *__restrict__ bin,
                                                       uint32_t *__restrict__ chunk_first) {
     __shared__ uint32_t s_tmp[4];
+    const int64_t n = d_n ? (int64_t)*d_n : n_max;
+    if ((int64_t)blockIdx.x * kTile >= n) return;  // whole block
     const int tid = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)tid * kItems;
     uint32_t cnt[kItems], id[kItems], sum = 0;
@@ -403,11 +413,12 @@ __global__ __launch_bounds__(kBlock) void k_globalize(const uint32_t *__restrict
 int64_t gsr_scan_blocks(int64_t n) { return (n + kTile - 1) / kTile; }
 
 hipError_t gsr_launch_scan_reduce(const uint32_t *perm, const uint2 *strip_rect, int64_t n,
-                                  uint32_t *partials, uint2 *rect_sorted, hipStream_t s) {
+                                  const uint32_t *d_n, uint32_t *partials, uint2 *rect_sorted,
+                                  hipStream_t s) {
     const int64_t nb = gsr_scan_blocks(n);
     if (nb == 0) return hipSuccess;
     hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(kBlock), 0, s, perm, strip_rect, n,
-                       partials, rect_sorted);
+                       d_n, partials, rect_sorted);
     return hipGetLastError();
 }
 
@@ -418,12 +429,13 @@ hipError_t gsr_launch_scan_partials(uint32_t *partials, int64_t nb, uint64_t *to
 }
 
 hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint2 *rect_sorted,
-                                const uint32_t *partials, int64_t n, const uint64_t *total,
-                                uint4 *bin, uint32_t *chunk_first, hipStream_t s) {
+                                const uint32_t *partials, int64_t n, const uint32_t *d_n,
+                                const uint64_t *total, uint4 *bin, uint32_t *chunk_first,
+                                hipStream_t s) {
     const int64_t nb = gsr_scan_blocks(n);
     if (nb == 0) return hipSuccess;
     hipLaunchKernelGGL(k_scan_down, dim3((unsigned)nb), dim3(kBlock), 0, s, perm, rect_sorted,
-                       partials, n, total, bin, chunk_first);
+                       partials, n, d_n, total, bin, chunk_first);
     return hipGetLastError();
 }
 

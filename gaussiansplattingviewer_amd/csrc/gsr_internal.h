@@ -240,10 +240,13 @@ hipError_t gsr_launch_index_to_i32(const uint32_t *vals, int64_t P, int32_t *out
 int64_t gsr_radix_hist_words(int64_t n);
 // shape: tile shape (waves x items per lane): 0 = 4x16, 1 = 16x16, 2 = 4x8, 3 = 8x8, 4 = 8x16,
 // 5 = 4x4 (items per lane a multiple of 4, >= 4 waves).
+// d_count (compacting mode, >= 2 passes, first_pass 0): keys equal to 0xFFFFFFFF are dropped
+// by pass 0, the count of the others is stored at *d_count (device) and only they are sorted
+// -- the first *d_count entries of the result.  digit_total then needs 256 words per pass.
 hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
                                 uint32_t **vals_alt, int64_t n, int begin_bit, int end_bit,
                                 uint32_t *hist, uint32_t *digit_total, hipStream_t s,
-                                int shape = 0, int first_pass = 0);
+                                int shape = 0, int first_pass = 0, uint32_t *d_count = nullptr);
 // k_rs_scan alone: per digit, exclusive scan of hist[d][0..nb) across tiles -> digit_total[d].
 hipError_t gsr_launch_digit_scan(uint32_t *hist, int64_t nb, uint32_t *digit_total,
                                  hipStream_t s);
@@ -276,16 +279,19 @@ hipError_t gsr_onesweep_sort(uint32_t **keys, uint32_t **vals, uint32_t **keys_a
 // Binning: offsets scan over depth-sorted strip tile counts, duplicate into (tile, id)
 // pairs, and tile ranges.
 int64_t gsr_scan_blocks(int64_t n);
-// also writes rect_sorted[e] = strip_rect[perm[e]]
+// also writes rect_sorted[e] = strip_rect[perm[e]].  d_n (optional): entries of perm to scan
+// (the compacting depth sort's count; n is then only the grid bound).
 hipError_t gsr_launch_scan_reduce(const uint32_t *perm, const uint2 *strip_rect, int64_t n,
-                                  uint32_t *partials, uint2 *rect_sorted, hipStream_t s);
+                                  const uint32_t *d_n, uint32_t *partials, uint2 *rect_sorted,
+                                  hipStream_t s);
 hipError_t gsr_launch_scan_partials(uint32_t *partials, int64_t nb, uint64_t *total,
                                     hipStream_t s);
 // bin[e] (e = depth rank, only for Gaussians with pairs) = {exclusive pair offset, Gaussian
 // id, x0 | width << 16, strip-local row0}
 hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint2 *rect_sorted,
-                                const uint32_t *partials, int64_t n, const uint64_t *total,
-                                uint4 *bin, uint32_t *chunk_first, hipStream_t s);
+                                const uint32_t *partials, int64_t n, const uint32_t *d_n,
+                                const uint64_t *total, uint4 *bin, uint32_t *chunk_first,
+                                hipStream_t s);
 int64_t gsr_duplicate_chunks(int64_t K);
 hipError_t gsr_launch_duplicate(const uint4 *bin, const uint32_t *chunk_first, int64_t K,
                                 uint32_t gx, uint32_t *tile_keys, uint32_t *tile_vals,

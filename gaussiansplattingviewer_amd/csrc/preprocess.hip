@@ -257,7 +257,7 @@ __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__
 // Colour of the Gaussians k_preprocess kept (radii > 0, as upstream computes colour only for
 // those): upstream computeColorFromSH, or colors_precomp copied.
 __device__ __forceinline__ void color_one(const GsrPreprocessArgs &a, int64_t idx) {
-    if (a.radii[idx] == 0) return;
+    if (a.rgb ? a.radii[idx] == 0 : a.strip_rect[idx].x == 0u) return;
     float3 col;
     if (a.colors_precomp) {
         col = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1],
@@ -294,7 +294,9 @@ __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
     for (int64_t wv = (int64_t)blockIdx.x * 4 + w; wv < n_waves; wv += wave_stride) {
         const int64_t base = wv * 64, idx = base + lane;
         const bool in = idx < a.P;
-        const bool vis = in && a.radii[idx] != 0;
+        // colour needed: Gaussians with pairs in this strip (the blend reads them), or every
+        // visible one when the caller asked for the rgb output (upstream semantics)
+        const bool vis = in && (a.rgb ? a.radii[idx] != 0 : a.strip_rect[idx].x != 0u);
         if (__ballot(vis) == 0ull) continue;
         if (!a.sh_vec4 || a.colors_precomp || a.D != 3) {
             if (vis) color_one(a, idx);

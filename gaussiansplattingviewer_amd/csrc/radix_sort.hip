@@ -37,34 +37,74 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kRadix = kRadixBins;
 
+// Element count of a pass.  The compacting depth sort (gsr_radix_sort_compact) learns its
+// count on the device: pass 0 drops the sentinel keys, pass 1's upsweep sums pass 0's digit
+// totals (sum_digits; block 0 stores the sum at n_out) and every later kernel reads it from
+// d_n.  Grids and the hist column stride stay sized for the host's upper bound.
+struct RsCount {
+    int64_t n_host;
+    const uint32_t *sum_digits;  // if set: n = sum of these 256 words
+    uint32_t *n_out;             // with sum_digits: block 0 stores n here
+    const uint32_t *d_n;         // else if set: n = *d_n
+};
+
+// All threads of the block call it (the sum_digits form reduces over 256 threads).
+template <int kThreads>
+__device__ __forceinline__ int64_t resolve_count(const RsCount &c, uint32_t *s_red) {
+    if (c.sum_digits) {
+        static_assert(kThreads >= kRadixBins, "one thread per digit");
+        const int tid = threadIdx.x;
+        uint32_t v = tid < kRadixBins ? c.sum_digits[tid] : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if ((tid & 63) == 0) s_red[tid >> 6] = v;
+        __syncthreads();
+        uint32_t n = 0;
+#pragma unroll
+        for (int i = 0; i < kThreads / 64; ++i) n += s_red[i];
+        __syncthreads();
+        if (c.n_out && blockIdx.x == 0 && tid == 0) *c.n_out = n;
+        return n;
+    }
+    if (c.d_n) return *c.d_n;
+    return c.n_host;
+}
+
 // Reduce-then-scan, parameterised by waves per block (kW = 4: 4096-key tiles for the
 // P-sized depth sort; kW = 16: 16384-key tiles and 1024-thread blocks for the K-sized tile
-// sort, so each digit's run in a tile is long enough for full-line stores).
-template <int kW, int kIt>
+// sort, so each digit's run in a tile is long enough for full-line stores).  nb = hist column
+// stride (tiles of the host's upper bound); kDrop: keys equal to kDropKey are not counted.
+template <int kW, int kIt, bool kDrop = false>
 __global__ __launch_bounds__(kW * 64) void k_rs_upsweep(const uint32_t *__restrict__ keys,
-                                                        int64_t n, int shift, uint32_t mask,
+                                                        const RsCount cnt, int shift,
+                                                        uint32_t mask,
                                                         uint32_t *__restrict__ hist, int64_t nb) {
     constexpr int kThreads = kW * 64, kT = kThreads * kIt;
     static_assert(kIt % 4 == 0, "full tiles are read as uint4");
     static_assert(kW >= 4, "the digit scans take one thread per digit (256)");
     __shared__ uint32_t s_hist[kW][kRadix];
+    __shared__ uint32_t s_red[kW];
     const int tid = threadIdx.x, w = tid >> 6;
+    const int64_t n = resolve_count<kThreads>(cnt, s_red);
+    const int64_t base = (int64_t)blockIdx.x * kT;
+    if (base >= n) return;  // whole block (the scan reads columns [0, ceil(n / kT)) only)
     for (int i = tid; i < kW * kRadix; i += kThreads) (&s_hist[0][0])[i] = 0;
     __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * kT;
+    auto add = [&](uint32_t key) {
+        if (!kDrop || key != kDropKey) atomicAdd(&s_hist[w][(key >> shift) & mask], 1u);
+    };
     if (base + kT <= n) {
         const uint4 *k4 = reinterpret_cast<const uint4 *>(keys + base);
 #pragma unroll
         for (int j = 0; j < kIt / 4; ++j) {
             const uint4 q = k4[j * kThreads + tid];
-            atomicAdd(&s_hist[w][(q.x >> shift) & mask], 1u);
-            atomicAdd(&s_hist[w][(q.y >> shift) & mask], 1u);
-            atomicAdd(&s_hist[w][(q.z >> shift) & mask], 1u);
-            atomicAdd(&s_hist[w][(q.w >> shift) & mask], 1u);
+            add(q.x);
+            add(q.y);
+            add(q.z);
+            add(q.w);
         }
     } else {
-        for (int64_t e = base + tid; e < n; e += kThreads)
-            atomicAdd(&s_hist[w][(keys[e] >> shift) & mask], 1u);
+        for (int64_t e = base + tid; e < n; e += kThreads) add(keys[e]);
     }
     __syncthreads();
     if (tid < kRadix) {
@@ -75,18 +115,21 @@ __global__ __launch_bounds__(kW * 64) void k_rs_upsweep(const uint32_t *__restri
     }
 }
 
-// One block per digit: exclusive scan of hist[d][0..nb) in place, total -> digit_total[d].
+// One block per digit: exclusive scan of hist[d][0..ceil(n / kT)) (column stride nb) in
+// place, total -> digit_total[d].
 __global__ __launch_bounds__(kBlock) void k_rs_scan(uint32_t *__restrict__ hist, int64_t nb,
-                                                    uint32_t *__restrict__ digit_total) {
+                                                    uint32_t *__restrict__ digit_total,
+                                                    const RsCount cnt, int64_t kT) {
     __shared__ uint32_t s_tmp[4];
+    const int64_t nb_act = cnt.d_n ? ((int64_t)*cnt.d_n + kT - 1) / kT : nb;
     uint32_t *h = hist + (int64_t)blockIdx.x * nb;
     uint32_t carry = 0;
-    for (int64_t start = 0; start < nb; start += kBlock * 4) {
+    for (int64_t start = 0; start < nb_act; start += kBlock * 4) {
         uint32_t v[4], sum = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int64_t e = start + threadIdx.x * 4 + i;
-            v[i] = e < nb ? h[e] : 0u;
+            v[i] = e < nb_act ? h[e] : 0u;
             sum += v[i];
         }
         uint32_t total;
@@ -94,7 +137,7 @@ __global__ __launch_bounds__(kBlock) void k_rs_scan(uint32_t *__restrict__ hist,
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int64_t e = start + threadIdx.x * 4 + i;
-            if (e < nb) h[e] = pre;
+            if (e < nb_act) h[e] = pre;
             pre += v[i];
         }
         carry += total;
@@ -102,18 +145,20 @@ __global__ __launch_bounds__(kBlock) void k_rs_scan(uint32_t *__restrict__ hist,
     if (threadIdx.x == 0) digit_total[blockIdx.x] = carry;
 }
 
-template <int kW, int kIt>
+template <int kW, int kIt, bool kDrop = false>
 __global__ __launch_bounds__(kW * 64) void k_rs_downsweep(
     const uint32_t *__restrict__ keys_in, const uint32_t *__restrict__ vals_in,
-    uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out, int64_t n, int shift,
-    int nbits, const uint32_t *__restrict__ hist, const uint32_t *__restrict__ digit_total,
-    int64_t nb) {
+    uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out, const RsCount cnt,
+    int shift, int nbits, const uint32_t *__restrict__ hist,
+    const uint32_t *__restrict__ digit_total, int64_t nb) {
     constexpr int kT = kW * 64 * kIt;
     __shared__ uint32_t s_keys[kT];
     __shared__ uint32_t s_vals[kT];
     __shared__ RadixTileSmem<kW, kIt> sm;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t n = cnt.d_n ? (int64_t)*cnt.d_n : cnt.n_host;
     const int64_t base = (int64_t)blockIdx.x * kT;
+    if (base >= n) return;  // whole block
     uint32_t k[kIt], v[kIt];
 #pragma unroll
     for (int j = 0; j < kIt; ++j) {
@@ -123,8 +168,9 @@ __global__ __launch_bounds__(kW * 64) void k_rs_downsweep(
         v[j] = valid ? vals_in[e] : 0u;
     }
     const int64_t rem = n - base;
-    radix_tile_scatter<kW, kIt>(k, v, rem < kT ? (int)rem : kT, shift, nbits, hist, nb,
-                                blockIdx.x, digit_total, keys_out, vals_out, sm, s_keys, s_vals);
+    radix_tile_scatter<kW, kIt, kDrop>(k, v, rem < kT ? (int)rem : kT, shift, nbits, hist, nb,
+                                       blockIdx.x, digit_total, keys_out, vals_out, sm, s_keys,
+                                       s_vals);
 }
 
 // ---- onesweep -----------------------------------------------------------------------------
@@ -334,7 +380,8 @@ hipError_t gsr_onesweep_sort(uint32_t **keys, uint32_t **vals, uint32_t **keys_a
 
 hipError_t gsr_launch_digit_scan(uint32_t *hist, int64_t nb, uint32_t *digit_total,
                                  hipStream_t s) {
-    hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, nb, digit_total);
+    hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, nb, digit_total,
+                       RsCount{nb, nullptr, nullptr, nullptr}, (int64_t)1);
     return hipGetLastError();
 }
 
@@ -343,41 +390,63 @@ int64_t gsr_radix_hist_words(int64_t n) {
     return (nb < 1 ? 1 : nb) * kRadix;
 }
 
-template <int kW, int kIt>
-static void rts_pass(const uint32_t *k, const uint32_t *v, uint32_t *ko, uint32_t *vo, int64_t n,
-                     int shift, int nbits, uint32_t *hist, uint32_t *digit_total, hipStream_t s) {
+template <int kW, int kIt, bool kDrop = false>
+static void rts_pass(const uint32_t *k, const uint32_t *v, uint32_t *ko, uint32_t *vo,
+                     const RsCount &up_cnt, const RsCount &cnt, int shift, int nbits,
+                     uint32_t *hist, uint32_t *digit_total, hipStream_t s) {
     const int64_t kT = (int64_t)kW * 64 * kIt;
-    const int64_t nb = (n + kT - 1) / kT;
+    const int64_t nb = (cnt.n_host + kT - 1) / kT;  // grid and hist column stride
+    if (nb == 0) return;
     const uint32_t mask = (1u << nbits) - 1u;
-    hipLaunchKernelGGL((k_rs_upsweep<kW, kIt>), dim3((unsigned)nb), dim3(kW * 64), 0, s, k, n,
-                       shift, mask, hist, nb);
-    hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, nb, digit_total);
-    hipLaunchKernelGGL((k_rs_downsweep<kW, kIt>), dim3((unsigned)nb), dim3(kW * 64), 0, s, k, v,
-                       ko, vo, n, shift, nbits, hist, digit_total, nb);
+    hipLaunchKernelGGL((k_rs_upsweep<kW, kIt, kDrop>), dim3((unsigned)nb), dim3(kW * 64), 0, s,
+                       k, up_cnt, shift, mask, hist, nb);
+    hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, nb, digit_total, cnt,
+                       kT);
+    hipLaunchKernelGGL((k_rs_downsweep<kW, kIt, kDrop>), dim3((unsigned)nb), dim3(kW * 64), 0, s,
+                       k, v, ko, vo, cnt, shift, nbits, hist, digit_total, nb);
+}
+
+template <int kW, int kIt>
+static void rts_sort(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt, uint32_t **vals_alt,
+                     int64_t n, const GsrRadixPlan &plan, int first_pass, uint32_t *hist,
+                     uint32_t *digit_total, uint32_t *d_count, hipStream_t s) {
+    for (int p = first_pass; p < plan.n; ++p) {
+        const int sh = plan.shift[p], nbits = plan.nbits[p];
+        if (!d_count) {
+            const RsCount c{n, nullptr, nullptr, nullptr};
+            rts_pass<kW, kIt>(*keys, *vals, *keys_alt, *vals_alt, c, c, sh, nbits, hist,
+                              digit_total, s);
+        } else if (p == 0) {  // drop the sentinel keys; pass 0's digit totals sum to the count
+            const RsCount c{n, nullptr, nullptr, nullptr};
+            rts_pass<kW, kIt, true>(*keys, *vals, *keys_alt, *vals_alt, c, c, sh, nbits, hist,
+                                    digit_total, s);
+        } else {  // pass 1's upsweep stores the count; everything else reads it
+            const RsCount up = p == 1 ? RsCount{n, digit_total, d_count, nullptr}
+                                      : RsCount{n, nullptr, nullptr, d_count};
+            const RsCount c{n, nullptr, nullptr, d_count};
+            rts_pass<kW, kIt>(*keys, *vals, *keys_alt, *vals_alt, up, c, sh, nbits, hist,
+                              digit_total + kRadix * p, s);
+        }
+        std::swap(*keys, *keys_alt);
+        std::swap(*vals, *vals_alt);
+    }
 }
 
 hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
                                 uint32_t **vals_alt, int64_t n, int begin_bit, int end_bit,
                                 uint32_t *hist, uint32_t *digit_total, hipStream_t s, int shape,
-                                int first_pass) {
-    if (n <= 1) return hipSuccess;
+                                int first_pass, uint32_t *d_count) {
+    if (n <= 1 && !d_count) return hipSuccess;
     const GsrRadixPlan plan = gsr_radix_plan(begin_bit, end_bit);
-    for (int p = first_pass; p < plan.n; ++p) {
-        const int sh = plan.shift[p], nb = plan.nbits[p];
-        switch (shape) {
-            case 1: rts_pass<16, 16>(*keys, *vals, *keys_alt, *vals_alt, n, sh, nb, hist, digit_total, s); break;
-            case 2: rts_pass<4, 8>(*keys, *vals, *keys_alt, *vals_alt, n, sh, nb, hist, digit_total, s); break;
-            case 3: rts_pass<8, 8>(*keys, *vals, *keys_alt, *vals_alt, n, sh, nb, hist, digit_total, s); break;
-            case 4: rts_pass<8, 16>(*keys, *vals, *keys_alt, *vals_alt, n, sh, nb, hist, digit_total, s); break;
-            case 5: rts_pass<4, 4>(*keys, *vals, *keys_alt, *vals_alt, n, sh, nb, hist, digit_total, s); break;
-            default: rts_pass<4, 16>(*keys, *vals, *keys_alt, *vals_alt, n, sh, nb, hist, digit_total, s); break;
-        }
-        uint32_t *t = *keys;
-        *keys = *keys_alt;
-        *keys_alt = t;
-        t = *vals;
-        *vals = *vals_alt;
-        *vals_alt = t;
+    if (d_count && (plan.n < 2 || first_pass != 0))
+        return hipErrorInvalidValue;  // the count is established by passes 0 and 1
+    switch (shape) {
+        case 1: rts_sort<16, 16>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, s); break;
+        case 2: rts_sort<4, 8>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, s); break;
+        case 3: rts_sort<8, 8>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, s); break;
+        case 4: rts_sort<8, 16>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, s); break;
+        case 5: rts_sort<4, 4>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, s); break;
+        default: rts_sort<4, 16>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, s); break;
     }
     return hipGetLastError();
 }

@@ -36,16 +36,21 @@ struct RadixTileSmem {
     static constexpr int kT = kW * 64 * kIt;
     uint32_t wcnt[kW][kRadixBins];
     uint32_t delta[kRadixBins];
-    uint32_t tmp[2 * kW];
+    uint32_t tmp[2 * kW + 1];
 };
 
 // Tile layout: wave w holds elements [w*kT/kW, (w+1)*kT/kW) of the tile, item j of lane l is
 // element w*kT/kW + j*64 + l.  Elements >= `valid` must carry key 0xFFFFFFFF (largest digit)
-// and are not written.  hist_tile = this tile's exclusive digit offset column entry
-// (hist[d * nb + tile]) as scanned by k_rs_scan; digit_total = per-digit totals.
+// and are not written.  hist[d * nb + tile] = this tile's exclusive digit offset as scanned by
+// k_rs_scan (nb: the column stride); digit_total = per-digit totals.
+// kDrop: every element whose key is kDropKey (0xFFFFFFFF) is dropped -- not ranked, counted or
+// written -- so the output is the stable, compacted sequence of the other elements (the
+// upsweep must not count them either).
 // s_keys / s_vals: kT words each (may alias storage the caller no longer needs: the first
 // write to them follows two block barriers).
-template <int kW, int kIt>
+constexpr uint32_t kDropKey = 0xFFFFFFFFu;
+
+template <int kW, int kIt, bool kDrop = false>
 __device__ __forceinline__ void radix_tile_scatter(
     const uint32_t (&k)[kIt], const uint32_t (&v)[kIt], int valid, int shift, int nbits,
     const uint32_t *__restrict__ hist, int64_t nb, uint32_t tile,
@@ -69,9 +74,11 @@ __device__ __forceinline__ void radix_tile_scatter(
             const uint64_t bal = __ballot(bit);
             m &= bit ? bal : ~bal;
         }
+        const bool keep = !kDrop || k[j] != kDropKey;
+        if (kDrop) m &= __ballot(keep);  // dropped lanes neither count nor take a rank
         const uint32_t prior = sm.wcnt[w][d];
         rank[j] = prior + (uint32_t)__popcll(m & lt_mask);
-        if (lane == 63 - __clzll(m)) sm.wcnt[w][d] = prior + (uint32_t)__popcll(m);
+        if (keep && lane == 63 - __clzll(m)) sm.wcnt[w][d] = prior + (uint32_t)__popcll(m);
     }
     __syncthreads();
 
@@ -89,6 +96,7 @@ __device__ __forceinline__ void radix_tile_scatter(
         uint32_t tile_total, all_total;
         const uint32_t local_start =
             blockw_exclusive_scan<kW>(d < kRadixBins ? sum : 0u, sm.tmp, tile_total);
+        if (kDrop && tid == 0) sm.tmp[2 * kW] = tile_total;
         const uint32_t digit_start = blockw_exclusive_scan<kW>(
             d < kRadixBins ? digit_total[d] : 0u, sm.tmp + kW, all_total);
         if (d < kRadixBins) {
@@ -104,13 +112,15 @@ __device__ __forceinline__ void radix_tile_scatter(
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kIt; ++j) {
+        if (kDrop && k[j] == kDropKey) continue;
         const uint32_t d = (k[j] >> shift) & mask;
         const uint32_t pos = sm.wcnt[w][d] + rank[j];
         s_keys[pos] = k[j];
         s_vals[pos] = v[j];
     }
     __syncthreads();
-    for (int i = tid; i < valid; i += kThreads) {
+    const int n_out = kDrop ? (int)sm.tmp[2 * kW] : valid;  // kept elements of the tile
+    for (int i = tid; i < n_out; i += kThreads) {
         const uint32_t kk = s_keys[i];
         const uint32_t g = sm.delta[(kk >> shift) & mask] + (uint32_t)i;
         keys_out[g] = kk;
