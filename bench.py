@@ -59,6 +59,9 @@ def parse():
                     help="GSR_OPT_DEPTH_SORT_SHAPE (tuning)")
     ap.add_argument("--onesweep", action="store_true", help="GSR_OPT_SORT_ONESWEEP (tuning)")
     ap.add_argument("--unfused", action="store_true", help="GSR_OPT_FUSED_BINNING=0 (tuning)")
+    ap.add_argument("--sim-strip", default=None, metavar="R/N",
+                    help="diagnostic, 1 GPU: render only strip R of an N-way partition (no "
+                         "gather) to estimate one rank's share of an N-GPU frame")
     ap.add_argument("--inline-color", action="store_true",
                     help="GSR_OPT_SPLIT_COLOR=0: colour inside the preprocess kernel (tuning)")
     ap.add_argument("--blend-blocks", action="store_true",
@@ -173,6 +176,11 @@ def main():
     W, H = scene.W, scene.H
     gy = (H + 15) // 16
     rows = strip_rows(gy, world, rank) if world > 1 else None
+    if args.sim_strip:
+        if world > 1:
+            raise SystemExit("--sim-strip is a single-process diagnostic")
+        sr, sn = (int(x) for x in args.sim_strip.split("/"))
+        rows = strip_rows(gy, sn, sr)
 
     # N > 1: each rank renders its strip of tile rows; rank 0 gathers the frame (RCCL).  The
     # gather of frame i runs asynchronously while frame i+1 renders (at most two frames in
@@ -290,7 +298,9 @@ def main():
         "config": {"workload": f"{args.config}: {P} Gaussians, {W}x{H}, SH degree {scene.deg}, "
                                f"{scene.cam_kind} camera",
                    "gaussians": P, "width": W, "height": H, "sh_degree": scene.deg,
-                   "parallelism": f"image strips x{world}" + (" + RCCL gather" if world > 1 else ""),
+                   "parallelism": (f"SIMULATED strip {args.sim_strip} (diagnostic, no gather)"
+                                   if args.sim_strip else
+                                   f"image strips x{world}" + (" + RCCL gather" if world > 1 else "")),
                    "blend_arithmetic": args.blend},
         "msplats_per_sec": round(P * fps / 1e6, 2),
         "frame_stats": {"P_frustum": P_f, "P_visible": P_v, "K_pairs_mean": round(K_mean, 1),
