@@ -283,8 +283,7 @@ __device__ __forceinline__ uint32_t xcd_work(uint32_t b, uint32_t group) {
 template <bool kFast>
 __global__ __launch_bounds__(64) void k_blend_q(const GsrBlendArgs a, uint32_t n_work,
                                                 uint32_t per_xcd) {
-    __shared__ StagedSplat s_spl[64 + 1];  // slot 64: opacity-0 pad
-    __shared__ uint16_t s_list[64 + 2];
+    __shared__ StagedSplat s_spl[64];
 
     const uint32_t b = blockIdx.x;
     const uint32_t work = xcd_work(b, a.xcd_group);
@@ -297,11 +296,6 @@ __global__ __launch_bounds__(64) void k_blend_q(const GsrBlendArgs a, uint32_t n
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
     const float pfx = (float)px, pfy = (float)py;
-    if (lane == 0) {
-        s_spl[64].g = make_float4(0.f, 0.f, 0.f, 0.f);
-        s_spl[64].q = make_float4(0.f, 0.f, 0.f, 0.f);
-        s_spl[64].e = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
 
     const uint2 range = a.ranges[tile];
     // done carried in the sign of T, as in k_blend
@@ -347,8 +341,6 @@ __global__ __launch_bounds__(64) void k_blend_q(const GsrBlendArgs a, uint32_t n
         T = acc ? test_T : (term ? -fabsf(T) : T);
         last_contributor = acc ? __float_as_uint(sp.e.y) : last_contributor;
     };
-    const char *lds = reinterpret_cast<const char *>(s_spl);
-    auto fetch = [&](uint32_t off) { return *reinterpret_cast<const StagedSplat *>(lds + off); };
     const float X0 = (float)qx0, Y0 = (float)qy0;
 
     // pipeline: records of chunk c+1 and ids of chunk c+2 are in flight while c composites
@@ -385,26 +377,26 @@ __global__ __launch_bounds__(64) void k_blend_q(const GsrBlendArgs a, uint32_t n
         }
         int count = __popcll(bal);
         if (count == 0) continue;
-        // list of byte offsets, padded to an even count with the opacity-0 slot
-        if (lane < count) s_list[lane] = (uint16_t)(lane * sizeof(StagedSplat));
+        // the compacted slots are the list (no index indirection); an odd count is padded with
+        // an opacity-0 splat in slot `count` (< 64 for an odd count)
         if (count & 1) {
-            if (lane == 0) s_list[count] = (uint16_t)(64 * sizeof(StagedSplat));
+            if (lane < 12) reinterpret_cast<float *>(&s_spl[count])[lane] = 0.0f;
             ++count;
         }
         // one wave: its LDS writes above complete before the reads below are served
 
         auto next2 = [&](int k) { return k + 2 < count ? k + 2 : count - 2; };
-        StagedSplat a0 = fetch(s_list[0]), a1 = fetch(s_list[1]);
+        StagedSplat a0 = s_spl[0], a1 = s_spl[1];
         for (int k = 0;;) {
             int kn = next2(k);
-            const StagedSplat b0 = fetch(s_list[kn]), b1 = fetch(s_list[kn + 1]);
+            const StagedSplat b0 = s_spl[kn], b1 = s_spl[kn + 1];
             composite(a0);
             composite(a1);
             k += 2;
             if (k >= count) break;
             kn = next2(k);
-            a0 = fetch(s_list[kn]);
-            a1 = fetch(s_list[kn + 1]);
+            a0 = s_spl[kn];
+            a1 = s_spl[kn + 1];
             composite(b0);
             composite(b1);
             k += 2;
