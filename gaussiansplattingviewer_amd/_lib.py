@@ -28,6 +28,7 @@ EXPORTED_SYMBOLS = (
     "gsr_abi_version", "gsr_last_error", "gsr_create", "gsr_destroy", "gsr_reserve",
     "gsr_forward", "gsr_get_binning", "gsr_mark_visible", "gsr_depth_argsort",
     "gsr_set_timing", "gsr_stage_times", "gsr_stage_name", "gsr_set_option",
+    "gsr_ply_probe", "gsr_ply_load",
 )
 
 
@@ -63,6 +64,14 @@ class GsrOutputs(ctypes.Structure):
     ]
 
 
+class GsrPlyInfo(ctypes.Structure):
+    _fields_ = [
+        ("P", ctypes.c_int64), ("sh_coeffs", ctypes.c_int32), ("binary", ctypes.c_int32),
+        ("bbox_min", ctypes.c_float * 3), ("bbox_max", ctypes.c_float * 3),
+        ("center", ctypes.c_float * 3),
+    ]
+
+
 _lock = threading.Lock()
 _lib = None
 _contexts: dict[int, ctypes.c_void_p] = {}
@@ -87,9 +96,12 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.gsr_stage_name.argtypes = [i32]
     lib.gsr_stage_name.restype = ctypes.c_char_p
     lib.gsr_set_option.argtypes = [vp, i32, i64]
+    lib.gsr_ply_probe.argtypes = [ctypes.c_char_p, ctypes.POINTER(GsrPlyInfo)]
+    lib.gsr_ply_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(GsrPlyInfo), vp, vp, vp, vp, vp,
+                                 i32, vp]
     for name in ("gsr_create", "gsr_reserve", "gsr_forward", "gsr_get_binning",
                  "gsr_mark_visible", "gsr_depth_argsort", "gsr_set_timing",
-                 "gsr_stage_times", "gsr_set_option"):
+                 "gsr_stage_times", "gsr_set_option", "gsr_ply_probe", "gsr_ply_load"):
         getattr(lib, name).restype = i32
 
 

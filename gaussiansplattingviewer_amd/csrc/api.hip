@@ -71,6 +71,7 @@ struct gsr_context {
     int blend_wave_quadrants = 1;
     int color_blocks = 512;    // grid cap of the overlapped colour pass
     uint32_t blend_xcd_group = 16;  // tuning (env GSR_BLEND_XCD_GROUP)
+    int blend_lean = 0;             // tuning (env GSR_BLEND_LEAN)
     int aux_low_priority = 1;  // second stream at the lowest priority
     bool serial_color = false; // tuning (env GSR_SERIAL_COLOR): join right after the fork
     bool late_K = false;       // tuning (env GSR_LATE_K): also sync on the scan's total
@@ -187,6 +188,9 @@ int bits_for(uint64_t max_value) {  // bits needed to represent every value <= m
 
 }  // namespace
 
+// The thread's last-error message for the other translation units (ply_loader.hip).
+int gsr_set_error(int code, const std::string &msg) { return fail(code, msg); }
+
 extern "C" {
 
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }
@@ -219,6 +223,8 @@ int gsr_create(gsr_context **out) {
     ctx->aux_low_priority = env_prio ? std::atoi(env_prio) : 1;
     const char *env_cb = std::getenv("GSR_COLOR_BLOCKS");    // tuning: grid cap, 0 = none
     if (env_cb) ctx->color_blocks = std::atoi(env_cb);
+    const char *env_ln = std::getenv("GSR_BLEND_LEAN");
+    if (env_ln) ctx->blend_lean = std::atoi(env_ln);
     const char *env_xg = std::getenv("GSR_BLEND_XCD_GROUP");
     if (env_xg) ctx->blend_xcd_group = (uint32_t)std::atoi(env_xg);
     ctx->serial_color = std::getenv("GSR_SERIAL_COLOR") != nullptr;
@@ -671,6 +677,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     ba.fast = ctx->fast;
     ba.wave_quadrants = ctx->blend_wave_quadrants;
     ba.xcd_group = ctx->blend_xcd_group;
+    ba.lean = ctx->blend_lean;
     ba.stamps = ctx->blend_stamps;
     GSR_HIP(gsr_launch_blend(ba, s), "blend launch");
     GSR_TRY(stage_end(6));

@@ -280,9 +280,11 @@ __device__ __forceinline__ uint32_t xcd_work(uint32_t b, uint32_t group) {
 // barriers cost ~40 % of wave time, measured with GSR_DEBUG_BLEND_STAMPS).  Record gathers
 // are software-pipelined: a chunk's records are loaded while the previous chunk is
 // composited, their ids one chunk earlier still.  Blocks are mapped XCD-aware (xcd_work).
-template <bool kFast>
-__global__ __launch_bounds__(64) void k_blend_q(const GsrBlendArgs a, uint32_t n_work,
-                                                uint32_t per_xcd) {
+// kLean: no record prefetch (only the next chunk's ids), so the kernel fits 64 VGPRs and
+// 8 waves per SIMD; the record gathers' latency is then left to the other waves.
+template <bool kFast, bool kLean = false>
+__global__ __launch_bounds__(64, kLean ? 8 : 1) void k_blend_q(const GsrBlendArgs a,
+                                                             uint32_t n_work, uint32_t per_xcd) {
     __shared__ StagedSplat s_spl[64];
 
     const uint32_t b = blockIdx.x;
@@ -345,15 +347,24 @@ __global__ __launch_bounds__(64) void k_blend_q(const GsrBlendArgs a, uint32_t n
 
     // pipeline: records of chunk c+1 and ids of chunk c+2 are in flight while c composites
     uint32_t i0 = range.x + (uint32_t)lane;
-    uint32_t id_next = i0 + 64u < range.y ? a.point_list[i0 + 64u] : 0u;
+    uint32_t id_next = i0 < range.y ? a.point_list[i0] : 0u;
     SplatRecord r_next;
-    if (i0 < range.y) r_next = a.records[a.point_list[i0]];
+    if (!kLean) {
+        if (i0 < range.y) r_next = a.records[id_next];
+        id_next = i0 + 64u < range.y ? a.point_list[i0 + 64u] : 0u;
+    }
     for (uint32_t start = range.x; start < range.y; start += 64) {
         const uint32_t idx = start + (uint32_t)lane;
         const bool valid = idx < range.y;
-        const SplatRecord r = r_next;
-        if (idx + 64u < range.y) r_next = a.records[id_next];
-        if (idx + 128u < range.y) id_next = a.point_list[idx + 128u];
+        SplatRecord r;
+        if (kLean) {
+            if (valid) r = a.records[id_next];
+            if (idx + 64u < range.y) id_next = a.point_list[idx + 64u];
+        } else {
+            r = r_next;
+            if (idx + 64u < range.y) r_next = a.records[id_next];
+            if (idx + 128u < range.y) id_next = a.point_list[idx + 128u];
+        }
 
         bool keep = valid;
         if (valid && a.cull)
@@ -723,7 +734,10 @@ hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s) {
         // grid: whole groups on every XCD (blocks past n_work exit)
         const uint32_t g = a.xcd_group ? a.xcd_group * 8u : 8u;
         const uint32_t per_xcd = (n_work + g - 1) / g * g / 8u;
-        if (a.fast)
+        if (a.fast && a.lean)
+            hipLaunchKernelGGL((k_blend_q<true, true>), dim3(8u * per_xcd), dim3(64), 0, s, a,
+                               n_work, per_xcd);
+        else if (a.fast)
             hipLaunchKernelGGL((k_blend_q<true>), dim3(8u * per_xcd), dim3(64), 0, s, a, n_work,
                                per_xcd);
         else

@@ -323,6 +323,7 @@ struct GsrBlendArgs {
     int fast;   // 1: folded-constant FMA arithmetic + raw v_exp_f32; 2: same, packed 2 px/lane
     int wave_quadrants;  // 1: one independent wave per (tile, quadrant) (k_blend_q)
     uint32_t xcd_group;  // work items per XCD round-robin group (0: plain block order)
+    int lean;            // fast mode: k_blend_q<true, true> (no record prefetch, 8 waves/SIMD)
     // diagnostics (env GSR_DEBUG_BLEND_STAMPS): per-phase s_memtime sums, see blend.hip
     unsigned long long *stamps;
 };

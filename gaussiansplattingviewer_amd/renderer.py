@@ -106,7 +106,9 @@ class HIPRenderer(GaussianRenderBase):
         self.radii = None
 
     def update_gaussian_data(self, gaus):
-        self.gaussians = gaus_hip_from_cpu(gaus, self.device)
+        """renderer_cuda.py:135-137 (host GaussianData -> device); a GaussianDataHIP already on
+        the device (e.g. ply.load_ply(path, device=...)) is used as is."""
+        self.gaussians = gaus if isinstance(gaus, GaussianDataHIP) else gaus_hip_from_cpu(gaus, self.device)
         self.raster_settings["sh_degree"] = int(np.round(np.sqrt(self.gaussians.sh_dim))) - 1
 
     def sort_and_update(self, camera, use_file=False, pose=None):

@@ -126,6 +126,29 @@ int gsr_mark_visible(gsr_context *ctx, const float *means3D, int64_t P, const fl
 int gsr_depth_argsort(gsr_context *ctx, const float *xyz, int64_t P, const float *view_host16,
                       int32_t *out_index, float *out_depth, void *stream);
 
+/* ---- PLY loader (replaces util_gau.load_ply, util_gau.py:63-125) ----
+ * Reads a 3D Gaussian Splatting PLY (binary little / big endian or ascii) whose vertex
+ * element has x y z, f_dc_0..2, 45 f_rest_* (SH degree 3), opacity, scale_0..2, rot_0..3, and
+ * returns the reference's activated data as SoA float32 arrays: xyz[P*3], rot[P*4]
+ * (normalised quaternion), scale[P*3] (exp), opacity[P] (sigmoid), sh[P*48] (DC, then the 15
+ * rest coefficients channel-interleaved), plus the bounding box and mean of the positions.
+ * gsr_ply_probe reads the header only (P, sh_coeffs = 16).  gsr_ply_load fills the caller's
+ * arrays: host memory when device == 0, device memory (uploaded on `stream`, synchronised
+ * before return) otherwise.  info->P must be 0 or the probed count.  Errors: GSR_E_INVALID with
+ * gsr_last_error() naming the problem (missing property, wrong f_rest count, short file). */
+typedef struct gsr_ply_info {
+    int64_t P;          /* vertices */
+    int32_t sh_coeffs;  /* 16 (degree 3, the only layout the reference loader accepts) */
+    int32_t binary;     /* 1 binary, 0 ascii */
+    float bbox_min[3];  /* util_gau.py:80-85: min / max / mean of xyz (gsr_ply_load) */
+    float bbox_max[3];
+    float center[3];
+} gsr_ply_info;
+
+int gsr_ply_probe(const char *path, gsr_ply_info *info);
+int gsr_ply_load(const char *path, gsr_ply_info *info, float *xyz, float *rot, float *scale,
+                 float *opacity, float *sh, int device, void *stream);
+
 /* Stage timing (HIP events on the forward's stream, no extra synchronisation).
  * gsr_set_timing(1) starts recording one event set per forward (a ring of the last 256);
  * gsr_stage_times waits for the last timed forward and writes the MEAN per-stage time (ms)
