@@ -71,7 +71,7 @@ struct gsr_context {
     int blend_wave_quadrants = 1;
     int color_blocks = 512;    // grid cap of the overlapped colour pass
     uint32_t blend_xcd_group = 16;  // tuning (env GSR_BLEND_XCD_GROUP)
-    int blend_lean = 0;             // tuning (env GSR_BLEND_LEAN)
+    int blend_lean = 1;             // tuning (env GSR_BLEND_LEAN=0: record prefetch, 7 waves)
     int aux_low_priority = 1;  // second stream at the lowest priority
     bool serial_color = false; // tuning (env GSR_SERIAL_COLOR): join right after the fork
     bool late_K = false;       // tuning (env GSR_LATE_K): also sync on the scan's total
