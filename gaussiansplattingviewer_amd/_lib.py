@@ -28,8 +28,12 @@ EXPORTED_SYMBOLS = (
     "gsr_abi_version", "gsr_last_error", "gsr_create", "gsr_destroy", "gsr_reserve",
     "gsr_forward", "gsr_get_binning", "gsr_mark_visible", "gsr_depth_argsort",
     "gsr_set_timing", "gsr_stage_times", "gsr_stage_name", "gsr_set_option",
-    "gsr_ply_probe", "gsr_ply_load",
+    "gsr_ply_probe", "gsr_ply_load", "gsr_disparity_colors", "gsr_pack_image",
 )
+
+GSR_PACK_RGBA_F32 = 0
+GSR_PACK_RGB8 = 1
+GSR_PACK_R16 = 2
 
 
 class GsrGaussians(ctypes.Structure):
@@ -99,7 +103,11 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.gsr_ply_probe.argtypes = [ctypes.c_char_p, ctypes.POINTER(GsrPlyInfo)]
     lib.gsr_ply_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(GsrPlyInfo), vp, vp, vp, vp, vp,
                                  i32, vp]
-    for name in ("gsr_create", "gsr_reserve", "gsr_forward", "gsr_get_binning",
+    lib.gsr_disparity_colors.argtypes = [vp, i64, ctypes.POINTER(ctypes.c_float),
+                                         ctypes.POINTER(ctypes.c_float), ctypes.c_float, vp, vp]
+    lib.gsr_pack_image.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                   ctypes.c_int32, vp, vp]
+    for name in ("gsr_disparity_colors", "gsr_pack_image", "gsr_create", "gsr_reserve", "gsr_forward", "gsr_get_binning",
                  "gsr_mark_visible", "gsr_depth_argsort", "gsr_set_timing",
                  "gsr_stage_times", "gsr_set_option", "gsr_ply_probe", "gsr_ply_load"):
         getattr(lib, name).restype = i32

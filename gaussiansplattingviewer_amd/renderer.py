@@ -102,6 +102,10 @@ class HIPRenderer(GaussianRenderBase):
             "debug": False,
         }
         self.tile_rows = tile_rows  # optional (begin, end) strip of 16-px tile rows
+        self.render_mod = 3
+        self._warned_mod = False
+        self._view_gl = None   # the last pose's GL view (math layout), for the disparity mode
+        self._proj_gl = None
         self.image = None
         self.radii = None
 
@@ -118,7 +122,20 @@ class HIPRenderer(GaussianRenderBase):
         self.raster_settings["scale_modifier"] = float(modifier)
 
     def set_render_mod(self, mod: int):
-        pass  # the CUDA backend ignores render modes too (renderer_cuda.py:145-146)
+        """Render modes of the GL backend (gau_vert.glsl / gau_frag.glsl; the viewer passes
+        g_render_mode - 3, main.py:1010-1014).  The CUDA backend ignores them
+        (renderer_cuda.py:145-146); this backend implements the two the stereo capture uses:
+        mod >= 0 caps the SH degree at mod ("SH:0~k", gau_vert.glsl:217-247) and mod == -1
+        renders the disparity image (per-Gaussian disparity grey, Gaussians scaled by 1.2,
+        gau_vert.glsl:152-156, 182-207).  The ball / billboard modes (-2, -3, -4) render as the
+        default mode, as in the CUDA backend, with a one-time warning."""
+        mod = int(mod)
+        if mod < -1 and not self._warned_mod:
+            import warnings
+            warnings.warn(f"render mode {mod} (ball / billboard shading) is GL-only; "
+                          "rendering the default SH colours", stacklevel=2)
+            self._warned_mod = True
+        self.render_mod = mod
 
     def set_render_reso(self, w, h):
         self.raster_settings["image_height"] = int(h)
@@ -132,43 +149,62 @@ class HIPRenderer(GaussianRenderBase):
         else:
             view_mat = camera.get_view_matrix(True)
         view_mat = np.array(view_mat, dtype=np.float32)
+        self._view_gl = view_mat.copy()
+        self._proj_gl = np.array(camera.get_project_matrix(), dtype=np.float32)
         view_mat[[0, 2], :] = -view_mat[[0, 2], :]
         proj = camera.get_project_matrix() @ view_mat
-        self.raster_settings["viewmatrix"] = torch.tensor(view_mat.T).float().to(self.device)
-        self.raster_settings["campos"] = torch.tensor(np.asarray(camera.position)).float().to(self.device)
-        self.raster_settings["projmatrix"] = torch.tensor(proj.T).float().to(self.device)
+        self.raster_settings["viewmatrix"] = self._upload(view_mat.T)
+        self.raster_settings["campos"] = self._upload(camera.position)
+        self.raster_settings["projmatrix"] = self._upload(proj.T)
+
+    def _upload(self, a) -> torch.Tensor:
+        # contiguous float32 on the host first: a transposed (strided) host tensor would make
+        # .to() stage it and launch a device-side permute copy for every matrix
+        return torch.from_numpy(np.ascontiguousarray(np.asarray(a), dtype=np.float32)).to(self.device)
 
     def update_camera_intrin(self, camera):
         view_matrix = np.array(camera.get_view_matrix(), dtype=np.float32)
         view_matrix[[0, 2], :] = -view_matrix[[0, 2], :]
         proj = camera.get_project_matrix() @ view_matrix
-        self.raster_settings["projmatrix"] = torch.tensor(proj.T).float().to(self.device)
+        self.raster_settings["projmatrix"] = self._upload(proj.T)
         hfovx, hfovy, focal = camera.get_htanfovxy_focal()
         self.raster_settings["tanfovx"] = hfovx
         self.raster_settings["tanfovy"] = hfovy
 
     def draw(self):
-        rs = GaussianRasterizationSettings(**self.raster_settings)
+        settings = dict(self.raster_settings)
         g = self.gaussians
+        shs, colors = g.sh, None
+        if self.render_mod == -1:
+            if self._view_gl is None:
+                raise RuntimeError("disparity mode needs update_camera_pose first")
+            from .stereo import DISPARITY_SCALE, disparity_colors
+            colors = disparity_colors(g.xyz, self._view_gl, self._proj_gl)
+            shs = None
+            settings["scale_modifier"] = settings["scale_modifier"] * DISPARITY_SCALE
+        elif self.render_mod >= 0:
+            settings["sh_degree"] = min(settings["sh_degree"], self.render_mod)
+        rs = GaussianRasterizationSettings(**settings)
         with torch.no_grad():
             if self.tile_rows is None:
                 img, radii = GaussianRasterizer(raster_settings=rs)(
-                    means3D=g.xyz, means2D=None, shs=g.sh, colors_precomp=None,
+                    means3D=g.xyz, means2D=None, shs=shs, colors_precomp=colors,
                     opacities=g.opacity, scales=g.scale, rotations=g.rot, cov3D_precomp=None)
             else:
                 res = rasterize_gaussians_native(
-                    rs.bg, g.xyz, None, g.opacity, g.scale, g.rot, rs.scale_modifier, None,
+                    rs.bg, g.xyz, colors, g.opacity, g.scale, g.rot, rs.scale_modifier, None,
                     rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height,
-                    rs.image_width, g.sh, rs.sh_degree, rs.campos, rs.prefiltered, rs.debug,
+                    rs.image_width, shs, rs.sh_degree, rs.campos, rs.prefiltered, rs.debug,
                     tile_rows=self.tile_rows)
                 img, radii = res.color, res.radii
         self.image, self.radii = img, radii
         return img
 
     def rgba(self) -> torch.Tensor:
-        """renderer_cuda.py:226-228: (3,H,W) -> (H,W,4) with alpha = 1."""
-        img = self.image.permute(1, 2, 0)
-        return torch.concat([img, torch.ones_like(img[..., :1])], dim=-1).contiguous()
+        """renderer_cuda.py:226-228: (3,H,W) -> (H,W,4) with alpha = 1 (one device pack
+        kernel, gsr_pack_image)."""
+        from .stereo import pack_image
+        return pack_image(self.image, "rgba_f32")
 
 
 # --- sort backend --------------------------------------------------------------------------

@@ -12,6 +12,12 @@
  *   gsr_depth_argsort  <- the per-frame depth sort backend `_sort_gaussian(gaus, view_mat)`
  *                         (renderer_ogl.py:10-19 cpu, :22-38 cupy, :41-53 torch), consumed by
  *                         OpenGLRenderer.sort_and_update (renderer_ogl.py:139-146).
+ *   gsr_ply_probe/load <- util_gau.load_ply (util_gau.py:63-125).
+ *   gsr_disparity_colors <- the disparity render mode (render_mod == -1) of the GL vertex
+ *                         shader, gau_vert.glsl:182-207, driven by main.py:862-868.
+ *   gsr_pack_image     <- the frame hand-offs: CHW -> HWC+alpha (renderer_cuda.py:226-228) and
+ *                         the capture readbacks glReadPixels RGB8 / R32F->uint16 with their
+ *                         row flips (main.py:855-879, 895-917).
  *
  * Conventions (plain pointers and sizes only; no torch or HIP types):
  *   - every array pointer is DEVICE memory unless the comment says host;
@@ -148,6 +154,28 @@ typedef struct gsr_ply_info {
 int gsr_ply_probe(const char *path, gsr_ply_info *info);
 int gsr_ply_load(const char *path, gsr_ply_info *info, float *xyz, float *rot, float *scale,
                  float *opacity, float *sh, int device, void *stream);
+
+/* ---- Stereo dataset outputs ----
+ * gsr_disparity_colors: colors[3*i..3*i+2] = d_i for every Gaussian, with
+ *   d = |(ndc_x(p) + 1)/2 - (ndc_x(p + (baseline, 0, 0)) + 1)/2|, ndc_x(q) = (P V [q;1]).x /
+ *   (P V [q;1]).w -- gau_vert.glsl:182-207.  view_host16 / proj_host16 are HOST row-major
+ *   (math-layout) 4x4 matrices: the GL view and projection (util.py:58-105), NOT the negated /
+ *   transposed upstream pair.  Render these colours as colors_precomp with scale_modifier x 1.2
+ *   (gau_vert.glsl:152-156) to get the viewer's disparity image.
+ * gsr_pack_image: chw = the rasterizer's (3,H,W) float image (format R16 reads channel 0 only);
+ *   output row r comes from input row (flip_rows ? H-1-r : r).
+ *     GSR_PACK_RGBA_F32: float[H][W][4], alpha 1 (renderer_cuda.py:226-228, no flip);
+ *     GSR_PACK_RGB8:     uint8[H][W][3] = round(clamp(v,0,1)*255) (GL unorm conversion);
+ *     GSR_PACK_R16:      uint16[H][W] = uint16(v*65535) (numpy astype: truncate, wrap). */
+enum {
+    GSR_PACK_RGBA_F32 = 0,
+    GSR_PACK_RGB8 = 1,
+    GSR_PACK_R16 = 2
+};
+int gsr_disparity_colors(const float *means3D, int64_t P, const float *view_host16,
+                         const float *proj_host16, float baseline, float *colors, void *stream);
+int gsr_pack_image(const float *chw, int32_t H, int32_t W, int32_t format, int32_t flip_rows,
+                   void *out, void *stream);
 
 /* Stage timing (HIP events on the forward's stream, no extra synchronisation).
  * gsr_set_timing(1) starts recording one event set per forward (a ring of the last 256);
