@@ -323,8 +323,10 @@ inline void activate(const double *v, const Layout &L, bool opacity_f32, Row &r)
 
 // Convert vertices [b, e) of a binary file into the SoA host arrays.  Only the 59 fields the
 // loader uses are decoded; little-endian float32 fields (the 3DGS files) take a direct load.
+// Vertices [b, e) -> output rows (i - base) of the five arrays.
 void convert_binary(const unsigned char *data, const Header &h, const Layout &L, int64_t b,
-                    int64_t e, float *xyz, float *rot, float *scale, float *opacity, float *sh) {
+                    int64_t e, int64_t base, float *xyz, float *rot, float *scale, float *opacity,
+                    float *sh) {
     const bool swap = h.format == Header::BBE;
     // field slots in `v` (indexed like Header::props, so activate() can use L unchanged)
     std::vector<int> need;
@@ -359,12 +361,84 @@ void convert_binary(const unsigned char *data, const Header &h, const Layout &L,
             }
         }
         activate(v.data(), L, op32, r);
-        std::memcpy(xyz + 3 * i, r.xyz, 12);
-        std::memcpy(rot + 4 * i, r.rot, 16);
-        std::memcpy(scale + 3 * i, r.scale, 12);
-        opacity[i] = r.opacity;
-        std::memcpy(sh + 48 * i, r.sh, 192);
+        const int64_t o = i - base;
+        std::memcpy(xyz + 3 * o, r.xyz, 12);
+        std::memcpy(rot + 4 * o, r.rot, 16);
+        std::memcpy(scale + 3 * o, r.scale, 12);
+        opacity[o] = r.opacity;
+        std::memcpy(sh + 48 * o, r.sh, 192);
     }
+}
+
+// Converts vertices [b, e) with up to 16 threads (contiguous sub-ranges).
+void convert_binary_parallel(const unsigned char *data, const Header &h, const Layout &L,
+                             int64_t b, int64_t e, int64_t base, float *xyz, float *rot,
+                             float *scale, float *opacity, float *sh) {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int64_t n = e - b;
+    const int64_t nt = std::min<int64_t>(std::min<unsigned>(hw, 16u), std::max<int64_t>(1, n / 65536));
+    if (nt == 1) {
+        convert_binary(data, h, L, b, e, base, xyz, rot, scale, opacity, sh);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int64_t t = 0; t < nt; ++t)
+        th.emplace_back(convert_binary, data, std::cref(h), std::cref(L), b + n * t / nt,
+                        b + n * (t + 1) / nt, base, xyz, rot, scale, opacity, sh);
+    for (auto &t : th) t.join();
+}
+
+// Binary file, float positions, device output: convert chunks of vertices straight into one of
+// two pinned staging slots (SoA within the slot) and DMA each slot to the five device arrays
+// while the next chunk converts -- the conversion (multi-threaded) and the upload overlap, and
+// no full-size host copy is made.  Positions are also kept on the host for the bbox / mean.
+int load_binary_to_device(const Mapped &m, const Header &h, const Layout &L, int64_t P,
+                          float *xyz, float *rot, float *scale, float *opacity, float *sh,
+                          hipStream_t s, std::vector<float> &host_xyz) {
+    constexpr int64_t kRows = 1 << 18;             // vertices per chunk (~59 MB of output)
+    constexpr int64_t kFloats = 3 + 4 + 3 + 1 + 48;
+    const int64_t rows = std::min<int64_t>(kRows, P);
+    float *pin = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void **>(&pin), 2 * (size_t)rows * kFloats * sizeof(float)) !=
+        hipSuccess) {
+        (void)hipGetLastError();
+        return ply_fail(GSR_E_NOMEM, "pinned staging allocation failed");
+    }
+    host_xyz.resize((size_t)P * 3);
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool ok = hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) == hipSuccess;
+    bool used[2] = {false, false};
+    int slot = 0;
+    for (int64_t b = 0; ok && b < P; b += rows) {
+        const int64_t e = std::min(P, b + rows), n = e - b;
+        if (used[slot]) ok = hipEventSynchronize(ev[slot]) == hipSuccess;
+        if (!ok) break;
+        float *sx = pin + (size_t)slot * rows * kFloats;
+        float *sr = sx + 3 * n, *ss = sr + 4 * n, *so = ss + 3 * n, *ssh = so + n;
+        convert_binary_parallel(m.p + h.data_offset, h, L, b, e, b, sx, sr, ss, so, ssh);
+        std::memcpy(host_xyz.data() + 3 * b, sx, (size_t)n * 12);
+        const struct {
+            float *dst;
+            const float *src;
+            int64_t k;
+        } parts[] = {{xyz, sx, 3}, {rot, sr, 4}, {scale, ss, 3}, {opacity, so, 1}, {sh, ssh, 48}};
+        for (const auto &pt : parts)
+            ok = ok && hipMemcpyAsync(pt.dst + pt.k * b, pt.src, (size_t)(pt.k * n) * sizeof(float),
+                                      hipMemcpyHostToDevice, s) == hipSuccess;
+        ok = ok && hipEventRecord(ev[slot], s) == hipSuccess;
+        used[slot] = true;
+        slot ^= 1;
+    }
+    ok = ok && hipStreamSynchronize(s) == hipSuccess;
+    for (hipEvent_t x : ev)
+        if (x) (void)hipEventDestroy(x);
+    (void)hipHostFree(pin);
+    if (!ok) {
+        (void)hipGetLastError();
+        return ply_fail(GSR_E_HIP, "upload of the PLY data failed");
+    }
+    return GSR_OK;
 }
 
 int convert_ascii(const Mapped &m, const Header &h, const Layout &L, float *xyz, float *rot,
@@ -456,7 +530,18 @@ int gsr_ply_load(const char *path, gsr_ply_info *info, float *xyz, float *rot, f
     info->P = P;
     info->sh_coeffs = 16;
     info->binary = h.format != Header::ASCII;
-    // host staging: the caller's arrays, or pinned buffers that are uploaded afterwards
+    // positions of any non-float type: keep the raw values for the bbox / mean
+    bool xyz_f32 = true;
+    for (int c = 0; c < 3; ++c) xyz_f32 = xyz_f32 && h.props[L.xyz[c]].type == PType::F32;
+    if (device && xyz_f32 && h.format != Header::ASCII && P > 0) {
+        std::vector<float> host_xyz;
+        GSR_TRY_PLY(load_binary_to_device(m, h, L, P, xyz, rot, scale, opacity, sh,
+                                          static_cast<hipStream_t>(stream), host_xyz));
+        bbox_center(host_xyz.data(), P, info->bbox_min, info->bbox_max, info->center);
+        return GSR_OK;
+    }
+    // host staging: the caller's arrays, or a host copy that is uploaded afterwards (ascii
+    // files and non-float positions)
     float *hx = xyz, *hr = rot, *hs = scale, *ho = opacity, *hsh = sh;
     std::vector<float> tmp;
     if (device) {
@@ -467,22 +552,11 @@ int gsr_ply_load(const char *path, gsr_ply_info *info, float *xyz, float *rot, f
         ho = hs + 3 * P;
         hsh = ho + P;
     }
-    // positions of any non-float type: keep the raw values for the bbox / mean
-    bool xyz_f32 = true;
-    for (int c = 0; c < 3; ++c) xyz_f32 = xyz_f32 && h.props[L.xyz[c]].type == PType::F32;
     std::vector<double> xyz_raw(xyz_f32 ? 0 : (size_t)P * 3);
     if (h.format == Header::ASCII) {
         GSR_TRY_PLY(convert_ascii(m, h, L, hx, hr, hs, ho, hsh, xyz_f32 ? nullptr : xyz_raw.data()));
     } else {
-        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        const int64_t nt = std::min<int64_t>(std::min<unsigned>(hw, 16u), std::max<int64_t>(1, P / 65536));
-        std::vector<std::thread> th;
-        for (int64_t t = 0; t < nt; ++t) {
-            const int64_t b = P * t / nt, e = P * (t + 1) / nt;
-            th.emplace_back(convert_binary, m.p + h.data_offset, std::cref(h), std::cref(L), b, e,
-                            hx, hr, hs, ho, hsh);
-        }
-        for (auto &t : th) t.join();
+        convert_binary_parallel(m.p + h.data_offset, h, L, 0, P, 0, hx, hr, hs, ho, hsh);
         if (!xyz_f32) {
             const bool swap = h.format == Header::BBE;
             for (int64_t i = 0; i < P; ++i)

@@ -27,6 +27,28 @@ def _raw(P, seed):
     return {k: np.asarray(a, np.float32) for k, a in v.items()}
 
 
+@pytest.mark.parametrize("P,fmt,types", [
+    (600_000, "binary_little_endian", None),          # pipelined upload: 3 chunks, ragged tail
+    (70_000, "binary_big_endian", None),
+    (30_000, "binary_little_endian", {"x": "double", "y": "double", "z": "double"}),
+    (5_000, "ascii", None),                           # host conversion, then upload
+])
+def test_device_load_equals_host_load(tmp_path, gpu, P, fmt, types):
+    path = tmp_path / "scene.ply"
+    raw = _raw(P, 12)
+    if types:
+        raw = {k: (v.astype(np.float64) if k in types else v) for k, v in raw.items()}
+    ply_oracle.write_ply(path, raw, fmt=fmt, types=types)
+    host, bbox_h, center_h = ply.load_ply(str(path))
+    dev, bbox_d, center_d = ply.load_ply(str(path), device=gpu)
+    torch.cuda.synchronize()
+    for name in ("xyz", "rot", "scale", "opacity"):
+        np.testing.assert_array_equal(getattr(dev, name).cpu().numpy(), getattr(host, name))
+    np.testing.assert_array_equal(dev.sh.cpu().numpy().reshape(-1, 48), host.sh)
+    np.testing.assert_array_equal(bbox_d, bbox_h)
+    np.testing.assert_array_equal(center_d, center_h)
+
+
 def test_device_load_equals_host_load_and_renders(tmp_path, gpu):
     path = tmp_path / "scene.ply"
     ply_oracle.write_ply(path, _raw(200_000, 11))
