@@ -53,6 +53,7 @@ struct gsr_context {
     // per-pair workspace
     DevBuf tile_keys, tile_vals, tile_keys_alt, tile_vals_alt;
     DevBuf ranges_local;
+    DevBuf tile_diff;  // difference-array partials + sum of the second-stream tile ranges
     uint64_t *h_total = nullptr;  // pinned: [K, look-back flag, K from the preprocess]
     unsigned long long *d_hostK = nullptr;  // device view of h_total + 2
     hipEvent_t kcount_ready = nullptr;  // the pair counts of this frame are on the host
@@ -68,6 +69,10 @@ struct gsr_context {
     int tile_sort_shape = 3;  // 8 waves x 8 keys/lane: fastest measured
     int depth_sort_shape = 3;  // 8x8: 78 us vs 89 for 4x16 at 1M keys (bench, round 1)
     int fused_binning = 1;    // duplicate fused with the first tile-sort pass
+    // tile ranges from the rects' per-tile counts on the second stream, after the colour
+    // (2; 1 = before it: the colour then overlaps the duplicate stage instead of the depth
+    // sort and the frame is ~2% slower; 0 = k_ranges on the main stream).  env GSR_AUX_RANGES
+    int aux_ranges = 2;
     int blend_wave_quadrants = 1;
     int color_blocks = 512;    // grid cap of the overlapped colour pass
     uint32_t blend_xcd_group = 16;  // tuning (env GSR_BLEND_XCD_GROUP)
@@ -225,6 +230,8 @@ int gsr_create(gsr_context **out) {
     if (env_cb) ctx->color_blocks = std::atoi(env_cb);
     const char *env_ln = std::getenv("GSR_BLEND_LEAN");
     if (env_ln) ctx->blend_lean = std::atoi(env_ln);
+    const char *env_ar = std::getenv("GSR_AUX_RANGES");
+    if (env_ar) ctx->aux_ranges = std::atoi(env_ar);
     const char *env_xg = std::getenv("GSR_BLEND_XCD_GROUP");
     if (env_xg) ctx->blend_xcd_group = (uint32_t)std::atoi(env_xg);
     ctx->serial_color = std::getenv("GSR_SERIAL_COLOR") != nullptr;
@@ -268,7 +275,8 @@ void gsr_destroy(gsr_context *ctx) {
                       &ctx->rect_sorted,   &ctx->pair_count,    &ctx->valid_count,
                       &ctx->sort_ctl,      &ctx->status,
                       &ctx->tile_keys,     &ctx->tile_vals,
-                      &ctx->tile_keys_alt, &ctx->tile_vals_alt, &ctx->ranges_local};
+                      &ctx->tile_keys_alt, &ctx->tile_vals_alt, &ctx->ranges_local,
+                      &ctx->tile_diff};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &set : ctx->ev)
@@ -447,6 +455,13 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
 
     GSR_TRY(reserve_P(ctx, P, s));
     GSR_TRY(grow(ctx, ctx->ranges_local, (size_t)std::max<uint64_t>(T_strip, 1) * 8, s));
+    // tile ranges on the second stream (from the rects' per-tile counts) when the strip's
+    // difference array fits in LDS; else k_ranges over the sorted keys on the main stream
+    const uint32_t diff_cells = gsr_tile_diff_cells(gx, rows_tiles);
+    const bool aux_ranges = ctx->split_color && !ctx->onesweep && ctx->fused_binning &&
+                            ctx->aux_ranges && diff_cells <= kTileDiffMaxCells;
+    if (aux_ranges)
+        GSR_TRY(grow(ctx, ctx->tile_diff, (size_t)(kTileDiffBlocks + 1) * diff_cells * 4, s));
 
     if (P == 0) {  // upstream returns the zero-initialised image without rendering
         GSR_HIP(hipMemsetAsync(out->color, 0, (size_t)3 * rows_out * W * sizeof(float), s),
@@ -528,7 +543,21 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         GSR_HIP(gsr_launch_count_pairs(pa, ctx->aux), "pair count launch");
         GSR_HIP(hipEventRecord(ctx->kcount_ready, ctx->aux), "hipEventRecord(pair count)");
         if (tmode == 1) GSR_HIP(hipEventRecord(evc[0], ctx->aux), "hipEventRecord");
+        if (aux_ranges && ctx->aux_ranges == 1) {
+            uint32_t *part = static_cast<uint32_t *>(ctx->tile_diff.p);
+            GSR_HIP(gsr_launch_tile_ranges_aux(pa.strip_rect, P, gx, rows_tiles, part,
+                                               part + (size_t)kTileDiffBlocks * diff_cells,
+                                               static_cast<uint2 *>(ctx->ranges_local.p), ctx->aux),
+                    "tile ranges launch");
+        }
         GSR_HIP(gsr_launch_color(pa, ctx->color_blocks, ctx->aux), "color launch");
+        if (aux_ranges && ctx->aux_ranges != 1) {
+            uint32_t *part = static_cast<uint32_t *>(ctx->tile_diff.p);
+            GSR_HIP(gsr_launch_tile_ranges_aux(pa.strip_rect, P, gx, rows_tiles, part,
+                                               part + (size_t)kTileDiffBlocks * diff_cells,
+                                               static_cast<uint2 *>(ctx->ranges_local.p), ctx->aux),
+                    "tile ranges launch");
+        }
         if (tmode == 1) GSR_HIP(hipEventRecord(evc[1], ctx->aux), "hipEventRecord");
         GSR_HIP(hipEventRecord(ctx->join, ctx->aux), "hipEventRecord(join)");
         // every exit from here on (errors included) leaves the caller's stream behind the
@@ -620,7 +649,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
                                              tplan.n ? tplan.nbits[0] : 0, hist, digit_total,
                                              tk_alt, tv_alt,
                                              static_cast<uint2 *>(ctx->ranges_local.p),
-                                             (uint32_t)T_strip, s),
+                                             aux_ranges ? 0u : (uint32_t)T_strip, s),
                     "duplicate launch");
             std::swap(tk, tk_alt);
             std::swap(tv, tv_alt);
@@ -647,10 +676,13 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     GSR_TRY(stage_end(4));
 
     // ---- 6. tile ranges ----------------------------------------------------------------------
-    if (!(fused && K > 0))  // else zeroed by k_dup_count
-        GSR_HIP(hipMemsetAsync(ctx->ranges_local.p, 0, T_strip * 8, s), "hipMemsetAsync(ranges)");
-    GSR_HIP(gsr_launch_ranges(tk, (int64_t)K, static_cast<uint32_t *>(ctx->ranges_local.p), s),
-            "ranges launch");
+    if (!aux_ranges) {  // else written on the second stream (joined below)
+        if (!(fused && K > 0))  // else zeroed by k_dup_count
+            GSR_HIP(hipMemsetAsync(ctx->ranges_local.p, 0, T_strip * 8, s),
+                    "hipMemsetAsync(ranges)");
+        GSR_HIP(gsr_launch_ranges(tk, (int64_t)K, static_cast<uint32_t *>(ctx->ranges_local.p), s),
+                "ranges launch");
+    }
     if (!join_guard.done) {  // the blend reads the colours: join the second stream here
         join_guard.done = true;
         GSR_HIP(hipStreamWaitEvent(s, ctx->join, 0), "hipStreamWaitEvent(join)");

@@ -471,6 +471,124 @@ hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_firs
     return hipGetLastError();
 }
 
+namespace {
+
+// ---- tile ranges from per-tile pair counts (second stream) ---------------------------------
+// The sorted pair list holds each tile's pairs contiguously in tile order, so ranges[t] =
+// [start_t, start_t + count_t) with start_t the exclusive scan of the per-tile pair counts --
+// which depend only on the Gaussians' tile rects, not on any sort.  They are computed on the
+// second stream while the main stream sorts: the rect of every Gaussian with pairs adds the
+// four corners of a 2D difference array (LDS atomics, per block), the blocks' arrays are summed,
+// and one block turns the sum into counts (row then column prefix sums) and ranges (an
+// exclusive scan in tile order).  Tiles without pairs get (0, 0), as upstream's memset leaves
+// them.  Replaces k_ranges, a pass over the K sorted keys on the main stream.
+constexpr int kDiffThreads = 1024;
+
+__global__ __launch_bounds__(kDiffThreads) void k_tile_diff(const uint2 *__restrict__ strip_rect,
+                                                            int64_t P, uint32_t gx, uint32_t rows,
+                                                            uint32_t *__restrict__ partial) {
+    extern __shared__ uint32_t s_diff[];
+    const uint32_t w1 = gx + 1, cells = w1 * (rows + 1);
+    for (uint32_t c = threadIdx.x; c < cells; c += kDiffThreads) s_diff[c] = 0u;
+    __syncthreads();
+    const int64_t b0 = P * blockIdx.x / gridDim.x, b1 = P * (blockIdx.x + 1) / gridDim.x;
+    for (int64_t i = b0 + threadIdx.x; i < b1; i += kDiffThreads) {
+        const uint2 r = strip_rect[i];
+        if (r.x == 0u) continue;  // no pairs in the strip (a rect with pairs has width > 0)
+        const uint32_t x0 = r.x & 0xFFFFu, x1 = x0 + (r.x >> 16);
+        const uint32_t y0 = r.y & 0xFFFFu, y1 = y0 + (r.y >> 16);
+        atomicAdd(&s_diff[y0 * w1 + x0], 1u);
+        atomicAdd(&s_diff[y0 * w1 + x1], 0xFFFFFFFFu);  // -1 (mod 2^32)
+        atomicAdd(&s_diff[y1 * w1 + x0], 0xFFFFFFFFu);
+        atomicAdd(&s_diff[y1 * w1 + x1], 1u);
+    }
+    __syncthreads();
+    uint32_t *dst = partial + (int64_t)blockIdx.x * cells;
+    for (uint32_t c = threadIdx.x; c < cells; c += kDiffThreads) dst[c] = s_diff[c];
+}
+
+__global__ __launch_bounds__(kBlock) void k_tile_diff_reduce(const uint32_t *__restrict__ partial,
+                                                             int nparts, uint32_t cells,
+                                                             uint32_t *__restrict__ diff) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= cells) return;
+    uint32_t v = 0;
+#pragma unroll 8
+    for (int b = 0; b < nparts; ++b) v += partial[(int64_t)b * cells + c];
+    diff[c] = v;
+}
+
+__device__ __forceinline__ void wave_prefix_line(uint32_t *s, uint32_t n, uint32_t stride,
+                                                 int lane) {
+    uint32_t carry = 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const uint32_t v = i < n ? s[i * stride] : 0u;
+        const uint32_t inc = wave_inclusive_scan(v) + carry;
+        if (i < n) s[i * stride] = inc;
+        carry = __shfl(inc, 63);
+    }
+}
+
+__global__ __launch_bounds__(kDiffThreads) void k_tile_ranges_from_diff(
+    const uint32_t *__restrict__ diff, uint32_t gx, uint32_t rows, uint2 *__restrict__ ranges) {
+    extern __shared__ uint32_t s_cnt[];
+    __shared__ uint32_t s_tmp[2 * (kDiffThreads / 64) + 1];
+    const uint32_t w1 = gx + 1, cells = w1 * (rows + 1);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int kWaves = kDiffThreads / 64;
+    for (uint32_t c = threadIdx.x; c < cells; c += kDiffThreads) s_cnt[c] = diff[c];
+    __syncthreads();
+    for (uint32_t y = wave; y < rows; y += kWaves) wave_prefix_line(s_cnt + y * w1, gx, 1, lane);
+    __syncthreads();
+    for (uint32_t x = wave; x < gx; x += kWaves) wave_prefix_line(s_cnt + x, rows, w1, lane);
+    __syncthreads();
+    // s_cnt[y * w1 + x] = pairs of tile (x, y); exclusive scan in tile order t = y * gx + x
+    const uint32_t T = gx * rows;
+    const uint32_t per = (T + kDiffThreads - 1) / kDiffThreads;
+    const uint32_t t0 = min(T, threadIdx.x * per), t1 = min(T, t0 + per);
+    uint32_t sum = 0;
+    for (uint32_t t = t0; t < t1; ++t) sum += s_cnt[(t / gx) * w1 + t % gx];
+    uint32_t total;
+    uint32_t start = blockw_exclusive_scan<kWaves>(sum, s_tmp, total);
+    for (uint32_t t = t0; t < t1; ++t) {
+        const uint32_t n = s_cnt[(t / gx) * w1 + t % gx];
+        ranges[t] = n ? make_uint2(start, start + n) : make_uint2(0u, 0u);
+        start += n;
+    }
+}
+
+}  // namespace
+
+uint32_t gsr_tile_diff_cells(uint32_t gx, uint32_t rows) { return (gx + 1) * (rows + 1); }
+
+hipError_t gsr_launch_tile_ranges_aux(const uint2 *strip_rect, int64_t P, uint32_t gx,
+                                      uint32_t rows, uint32_t *partial, uint32_t *diff,
+                                      uint2 *ranges, hipStream_t s) {
+    const uint32_t cells = gsr_tile_diff_cells(gx, rows);
+    const size_t lds = (size_t)cells * 4;
+    if (cells > kTileDiffMaxCells) return hipErrorInvalidValue;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_tile_diff),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           kTileDiffMaxCells * 4);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_tile_ranges_from_diff),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    kTileDiffMaxCells * 4);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(k_tile_diff, dim3(kTileDiffBlocks), dim3(kDiffThreads), lds, s, strip_rect,
+                       P, gx, rows, partial);
+    hipLaunchKernelGGL(k_tile_diff_reduce, dim3((cells + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                       partial, kTileDiffBlocks, cells, diff);
+    hipLaunchKernelGGL(k_tile_ranges_from_diff, dim3(1), dim3(kDiffThreads), lds, s, diff, gx,
+                       rows, ranges);
+    return hipGetLastError();
+}
+
 hipError_t gsr_launch_ranges(const uint32_t *tile_keys, int64_t K, uint32_t *ranges,
                              hipStream_t s) {
     if (K == 0) return hipSuccess;

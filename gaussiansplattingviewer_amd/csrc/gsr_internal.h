@@ -306,6 +306,16 @@ hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_firs
                                     uint2 *ranges_zero, uint32_t n_ranges, hipStream_t s);
 hipError_t gsr_launch_ranges(const uint32_t *tile_keys, int64_t K, uint32_t *ranges,
                              hipStream_t s);
+// Tile ranges from the Gaussians' strip tile rects alone (no sorted keys): per-tile pair
+// counts via a 2D difference array, then an exclusive scan; runs on the second stream.
+// partial: kTileDiffBlocks * cells words, diff: cells words, cells = gsr_tile_diff_cells(...)
+// <= kTileDiffMaxCells (the difference array lives in LDS).
+constexpr int kTileDiffBlocks = 64;
+constexpr uint32_t kTileDiffMaxCells = 38912;  // 152 KiB of LDS
+uint32_t gsr_tile_diff_cells(uint32_t gx, uint32_t rows);
+hipError_t gsr_launch_tile_ranges_aux(const uint2 *strip_rect, int64_t P, uint32_t gx,
+                                      uint32_t rows, uint32_t *partial, uint32_t *diff,
+                                      uint2 *ranges, hipStream_t s);
 hipError_t gsr_launch_globalize_tiles(const uint32_t *local, int64_t K, uint32_t offset,
                                       uint32_t *global, hipStream_t s);
 
