@@ -3,7 +3,11 @@
 Headline workload (BASELINE.json configs[2] = SURVEY.md §8(d) C3): 1M synthetic Gaussians,
 SH degree 3, 1920x1080, static camera, inputs resident in HBM.  One step = one full frame:
 preprocess (EWA + SH) -> device radix depth sort -> binning -> tile sort -> ranges -> blend,
-including the per-frame K readback the algorithm needs.  With --gpus N (one process per GPU,
+including the per-frame K readback the algorithm needs.  Two frames are in flight by
+default (--inflight, `FramePipeline`: frame i on stream / context slot i % 2, so the next
+frame's latency-bound preprocess and sort overlap this frame's VALU-bound blend; every frame
+is still rendered in full and bit-identically); `serial_ms_per_frame` reports one frame at a
+time.  With --gpus N (one process per GPU,
 launched by torch.distributed.run) the frame's 16-px tile rows are split into N strips, every
 rank renders its strip and rank 0 gathers the frame over RCCL (strong scaling: the frame is
 fixed, N grows).
@@ -33,6 +37,7 @@ from gaussiansplattingviewer_amd import _lib  # noqa: E402
 from gaussiansplattingviewer_amd.camera import cuda_camera_inputs, orbit_eye, static_camera  # noqa: E402
 from gaussiansplattingviewer_amd.gaussian_data import synthetic_gaussians  # noqa: E402
 from gaussiansplattingviewer_amd.rasterizer import rasterize_gaussians_native  # noqa: E402
+from gaussiansplattingviewer_amd.pipeline import FramePipeline  # noqa: E402
 from gaussiansplattingviewer_amd.strips import StripGather, strip_rows  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
@@ -69,6 +74,9 @@ def parse():
     ap.add_argument("--blend", default="fast", choices=["exact", "fast", "packed"],
                     help="blend arithmetic: GSR_OPT_BLEND_FAST (default) or upstream's exact "
                          "operation order")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="frames in flight (FramePipeline: own stream + context slot each); "
+                         "1 = serial forwards")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="minimum CPU-oracle time to sample for cpu_baseline")
     return ap.parse_args()
@@ -92,12 +100,12 @@ class Scene:
             view, proj, campos, tx, ty = cuda_camera_inputs(static_camera(W, H, eye))
             self.cams.append((up(view), up(proj), up(campos), tx, ty, (view, proj, campos)))
 
-    def render(self, step, tile_rows=None):
+    def render(self, step, tile_rows=None, slot=0, out_color=None):
         view, proj, campos, tx, ty, _ = self.cams[step % len(self.cams)]
         return rasterize_gaussians_native(self.bg, self.xyz, None, self.opacity, self.scale,
                                           self.rot, 1.0, None, view, proj, tx, ty, self.H, self.W,
                                           self.sh, self.deg, campos, False, False,
-                                          tile_rows=tile_rows)
+                                          tile_rows=tile_rows, slot=slot, out_color=out_color)
 
 
 # Measured HBM traffic per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate PMC passes;
@@ -105,7 +113,7 @@ class Scene:
 # each stage's roofline refers to.  The bench cannot read PMC counters itself; the profile is
 # of this same command (c3, default options).
 TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r01_c3_v8_kernels.json")
-STAGE_KERNEL = {"blend": "k_blend_q<true>", "preprocess": "k_preprocess<false>",
+STAGE_KERNEL = {"blend": "k_blend_q<true", "preprocess": "k_preprocess<false>",
                 "color": "k_color", "depth_sort": None, "duplicate": "k_dup_scatter",
                 "tile_sort": None, "scan": None, "ranges": "k_ranges"}
 
@@ -114,7 +122,9 @@ def measured_traffic(stage, config, default_opts):
     if config != "c3" or not default_opts or not os.path.exists(TRAFFIC_PROFILE):
         return None, None
     k = STAGE_KERNEL.get(stage)
-    rec = json.load(open(TRAFFIC_PROFILE)).get(k) if k else None
+    kernels = json.load(open(TRAFFIC_PROFILE))
+    # kernel names are matched by prefix (template arguments vary between builds)
+    rec = next((v for name, v in kernels.items() if name.startswith(k)), None) if k else None
     if not rec or rec.get("read_bytes_x2") is None or rec.get("write_bytes") is None:
         return None, None
     return int(rec["read_bytes_x2"] + rec["write_bytes"]), os.path.relpath(TRAFFIC_PROFILE, REPO)
@@ -185,14 +195,21 @@ def main():
     # N > 1: each rank renders its strip of tile rows; rank 0 gathers the frame (RCCL).  The
     # gather of frame i runs asynchronously while frame i+1 renders (at most two frames in
     # flight); the last frame's gather completes inside the timed region.
-    gather = StripGather(H, W, world, rank, device=dev) if world > 1 else None
+    gather = (StripGather(H, W, world, rank, device=dev, depth=args.inflight + 1)
+              if world > 1 else None)
+    # frames in flight: frame i renders on stream i % D with context slot i % D, so the next
+    # frame's latency-bound preprocess / sort / binning overlap this frame's blend
+    pipe = FramePipeline(args.inflight, dev)
 
     def step(i):
-        res = scene.render(i, rows)
-        if gather is not None:
-            if gather.pending:
-                gather.finish()
-            gather.submit(res.color)
+        with pipe.frame() as slot:
+            if gather is not None:
+                if len(gather.pending) == len(gather.slots) - 1:
+                    gather.finish()
+                res = scene.render(i, rows, slot, out_color=gather.next_buffer())
+                gather.submit(res.color)
+            else:
+                res = scene.render(i, rows, slot)
         return res
 
     def drain():
@@ -200,23 +217,23 @@ def main():
             gather.finish()
 
     lib = _lib.load_library()
-    ctx = _lib.context(local)
-    _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_BLEND_FAST,
-                                  {"exact": 0, "fast": 1, "packed": 2}[args.blend]),
-               "gsr_set_option")
-    if args.depth_sort_shape is not None:
-        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_DEPTH_SORT_SHAPE, args.depth_sort_shape),
-                   "opt")
-    if args.sort_shape is not None:
-        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_TILE_SORT_SHAPE, args.sort_shape), "opt")
-    if args.blend_blocks:
-        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_BLEND_WAVE_QUADRANTS, 0), "opt")
-    if args.inline_color:
-        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_SPLIT_COLOR, 0), "opt")
-    if args.unfused:
-        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_FUSED_BINNING, 0), "opt")
-    if args.onesweep:
-        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_SORT_ONESWEEP, 1), "opt")
+    ctxs = [_lib.context(local, slot) for slot in range(args.inflight)]
+    ctx = ctxs[0]  # stage timing is read from slot 0 (every D-th frame)
+    for c in ctxs:
+        opt = lambda o, v: _lib.check(lib.gsr_set_option(c, o, v), "gsr_set_option")  # noqa: E731
+        opt(_lib.GSR_OPT_BLEND_FAST, {"exact": 0, "fast": 1, "packed": 2}[args.blend])
+        if args.depth_sort_shape is not None:
+            opt(_lib.GSR_OPT_DEPTH_SORT_SHAPE, args.depth_sort_shape)
+        if args.sort_shape is not None:
+            opt(_lib.GSR_OPT_TILE_SORT_SHAPE, args.sort_shape)
+        if args.blend_blocks:
+            opt(_lib.GSR_OPT_BLEND_WAVE_QUADRANTS, 0)
+        if args.inline_color:
+            opt(_lib.GSR_OPT_SPLIT_COLOR, 0)
+        if args.unfused:
+            opt(_lib.GSR_OPT_FUSED_BINNING, 0)
+        if args.onesweep:
+            opt(_lib.GSR_OPT_SORT_ONESWEEP, 1)
 
     # Warmup (also sizes the workspace so the timed loop never allocates).
     for i in range(args.warmup):
@@ -245,11 +262,23 @@ def main():
     _lib.check(lib.gsr_stage_times(ctx, buf, len(names)), "gsr_stage_times")
     blend_ms_timed = float(buf[names.index("blend")])
 
-    # Per-stage breakdown (events at every stage boundary), untimed.
+    # Serial frame rate: one frame in flight (slot 0, the caller's stream, no gather) -- the
+    # frame time of a viewer that renders each frame before starting the next.
+    torch.cuda.synchronize()
+    n_serial = min(args.steps, 100)
+    t1 = time.perf_counter()
+    for i in range(n_serial):
+        scene.render(i, rows)
+    torch.cuda.synchronize()
+    serial_ms = 1e3 * (time.perf_counter() - t1) / n_serial
+
+    # Per-stage breakdown (events at every stage boundary), untimed: serial forwards on
+    # slot 0 (no frame overlap, no gather), so each stage's events bracket that stage alone.
     _lib.check(lib.gsr_set_timing(ctx, 1), "gsr_set_timing")
+    torch.cuda.synchronize()
     for i in range(min(args.steps, 30)):
-        step(i)
-    drain()
+        scene.render(i, rows)
+    torch.cuda.synchronize()
     _lib.check(lib.gsr_stage_times(ctx, buf, len(names)), "gsr_stage_times")
     _lib.check(lib.gsr_set_timing(ctx, 0), "gsr_set_timing")
     stage_ms = {n: float(buf[i]) for i, n in enumerate(names)}
@@ -306,9 +335,12 @@ def main():
         "frame_stats": {"P_frustum": P_f, "P_visible": P_v, "K_pairs_mean": round(K_mean, 1),
                         "tiles": T_strip},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
-        "stage_ms_note": "HIP events at every stage boundary, separate 30-frame pass (each "
-                         "event adds a few us); the timed region records the blend's two "
-                         "events only",
+        "stage_ms_note": "HIP events at every stage boundary, separate 30-frame serial pass "
+                         "(each event adds a few us); the timed region records the blend's "
+                         "two events only",
+        "inflight": args.inflight,
+        "serial_ms_per_frame": round(serial_ms, 4),
+        "serial_note": "one frame in flight at a time (no FramePipeline overlap), this rank",
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                      "traffic": traffic,

@@ -140,13 +140,18 @@ def check(rc: int, what: str) -> int:
     return rc
 
 
-def context(device_index: int) -> ctypes.c_void_p:
-    """The process-wide gsr_context of a device (created on first use, on that device)."""
+def context(device_index: int, slot: int = 0) -> ctypes.c_void_p:
+    """The process-wide gsr_context of a device (created on first use, on that device).
+
+    `slot` selects one of several independent contexts per device (own workspace, own
+    second stream): frames rendered through different slots on different streams may be in
+    flight at the same time (`pipeline.FramePipeline`)."""
     import torch
 
     lib = load_library()
+    key = (int(device_index), int(slot))
     with _lock:
-        ctx = _contexts.get(device_index)
+        ctx = _contexts.get(key)
         if ctx is not None:
             return ctx
         if not torch.cuda.is_available():
@@ -155,7 +160,7 @@ def context(device_index: int) -> ctypes.c_void_p:
         with torch.cuda.device(device_index):
             ctx = ctypes.c_void_p()
             check(lib.gsr_create(ctypes.byref(ctx)), "gsr_create")
-        _contexts[device_index] = ctx
+        _contexts[key] = ctx
         return ctx
 
 

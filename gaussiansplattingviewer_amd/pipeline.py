@@ -1,0 +1,75 @@
+"""Frames in flight: overlap the forward of frame i+1 with the end of frame i on one device.
+
+The reference draws one frame at a time on the legacy default stream (renderer_cuda.py:205-258,
+`cu.cudaStreamLegacy` at :231), so the GPU idles whenever the frame's critical path is
+latency-bound.  On MI355X the two halves of a frame have opposite profiles: the preprocess and
+the depth sort are short dependent launches that leave most of the 256 CUs idle, while the
+blend saturates the VALUs of every CU.  `FramePipeline` gives each in-flight frame its own
+stream and its own `gsr_context` slot (workspace + second stream, `_lib.context(dev, slot)`),
+so the next frame's preprocess / sort / binning fill the CUs the current blend leaves free.
+Every frame is still rendered completely and bit-identically to a serial forward (tested):
+only the order in which the GPU interleaves independent frames changes, as in a swap chain.
+"""
+from __future__ import annotations
+
+import torch
+
+
+class FramePipeline:
+    """Round-robin over `depth` (stream, context slot) pairs of one device.
+
+    Usage::
+
+        pipe = FramePipeline(depth=2, device=dev)
+        for cam in cameras:
+            with pipe.frame() as slot:          # enters the frame's stream
+                res = rasterize_gaussians_native(..., slot=slot)
+            ...
+        pipe.synchronize()
+
+    Frame i runs on stream i % depth; slot 0 is the caller's current stream, so depth=1 is the
+    serial forward.  A consumer on another stream must order itself after the frame
+    (`wait(stream_of_frame)`); `torch.cuda.synchronize()` waits for all of them.
+    """
+
+    def __init__(self, depth: int = 2, device=None):
+        if depth < 1:
+            raise ValueError("depth must be >= 1")
+        dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.device = dev
+        self.depth = depth
+        self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
+                                                            for _ in range(depth - 1)]
+        self.count = 0
+
+    def frame(self):
+        """Context manager for the next frame: enters its stream, yields its context slot."""
+        slot = self.count % self.depth
+        self.count += 1
+        return _FrameScope(self.streams[slot], slot)
+
+    @property
+    def last_stream(self) -> torch.cuda.Stream:
+        return self.streams[(self.count - 1) % self.depth]
+
+    def wait_last(self, stream: torch.cuda.Stream | None = None) -> None:
+        """Order `stream` (default: the current stream) after the most recent frame."""
+        (stream or torch.cuda.current_stream(self.device)).wait_stream(self.last_stream)
+
+    def synchronize(self) -> None:
+        for s in self.streams:
+            s.synchronize()
+
+
+class _FrameScope:
+    def __init__(self, stream, slot):
+        self.stream, self.slot = stream, slot
+        self._cm = None
+
+    def __enter__(self) -> int:
+        self._cm = torch.cuda.stream(self.stream)
+        self._cm.__enter__()
+        return self.slot
+
+    def __exit__(self, *exc):
+        return self._cm.__exit__(*exc)

@@ -68,13 +68,17 @@ class ForwardResult(NamedTuple):
 def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, rotations,
                                scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tanfovx,
                                tanfovy, image_height, image_width, sh, degree, campos, prefiltered,
-                               debug, *, tile_rows=None, extras=(), stream=None) -> ForwardResult:
+                               debug, *, tile_rows=None, extras=(), stream=None, slot=0,
+                               out_color=None) -> ForwardResult:
     """Same arguments, order and validation as upstream `_C.rasterize_gaussians`.
 
     Extensions (keyword-only, for the strip partition and the parity tests):
       tile_rows -- (begin, end) 16-px tile rows to render; the image is then strip-local;
       extras    -- names of intermediates to return: depths, means2D, conic_opacity, rgb,
-                   tiles_touched, final_T, n_contrib.
+                   tiles_touched, final_T, n_contrib;
+      stream    -- HIP stream handle (default: torch's current stream);
+      slot      -- context slot (`_lib.context`): forwards in different slots may overlap;
+      out_color -- preallocated contiguous f32 (3, rows, W) output (e.g. a gather buffer).
     """
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
@@ -110,7 +114,14 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
             raise RuntimeError(f"tile_rows {tile_rows} outside [0, {gy}]")
 
     f32 = dict(dtype=torch.float32, device=device)
-    color = torch.empty((3, rows, W), **f32)
+    if out_color is None:
+        color = torch.empty((3, rows, W), **f32)
+    else:
+        if (out_color.dtype != torch.float32 or not out_color.is_contiguous() or
+                tuple(out_color.shape) != (3, rows, W) or out_color.device != device):
+            raise RuntimeError(f"out_color must be a contiguous float32 (3, {rows}, {W}) tensor "
+                               f"on {device}")
+        color = out_color
     radii = torch.empty((P,), dtype=torch.int32, device=device)
     ext = {}
     for name in extras:
@@ -147,7 +158,7 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
     if stream is None:
         stream = torch.cuda.current_stream(device).cuda_stream
     lib = _lib.load_library()
-    ctx = _lib.context(dev_index)
+    ctx = _lib.context(dev_index, slot)
     with torch.cuda.device(dev_index):
         _lib.check(lib.gsr_forward(ctx, ctypes.byref(g), ctypes.byref(st), ctypes.byref(out),
                                    ctypes.c_void_p(stream)), "gsr_forward")

@@ -66,8 +66,11 @@ class StripGather:
     frame and returns it on rank 0 (None elsewhere).  Submitting frame i+1 before finishing
     frame i overlaps the gather with the next render, as a display swap chain would.
 
-    Buffers are allocated once: a padded send strip per in-flight frame and, on rank 0, the
-    (world, 3, hmax, W) receive block; the frame is assembled with one `cat` of the valid rows.
+    Buffers are allocated once: a flat send buffer per in-flight frame holding the strip's
+    (3, rows_me, W) planes back to back (padded to the tallest strip), and on rank 0 the
+    (world, 3 * hmax * W) receive block; the frame is assembled with one `cat`.
+    `next_buffer()` hands out the next send buffer as a (3, rows_me, W) view, so a renderer
+    can write its strip straight into it (`submit` then moves no bytes on this rank).
     """
 
     def __init__(self, H: int, W: int, world: int, rank: int, dtype=torch.float32,
@@ -77,24 +80,41 @@ class StripGather:
         self.layout = [strip_pixel_rows(strip_rows(gy, world, r), H) for r in range(world)]
         self.hmax = max(rows for _, rows in self.layout)
         self.rows_me = self.layout[rank][1]
+        n = 3 * self.hmax * W
         self.slots = [{
-            "send": torch.zeros((3, self.hmax, W), dtype=dtype, device=device),
-            "recv": (torch.empty((world, 3, self.hmax, W), dtype=dtype, device=device)
+            "send": torch.zeros((n,), dtype=dtype, device=device),
+            "recv": (torch.empty((world, n), dtype=dtype, device=device)
                      if rank == 0 else None),
+            "work": None,
         } for _ in range(depth)]
         self.next_slot = 0
         self.pending = []  # (slot, work)
+
+    def _strip_view(self, flat: torch.Tensor, rows: int) -> torch.Tensor:
+        return flat[:3 * rows * self.W].view(3, rows, self.W)
+
+    def next_buffer(self) -> torch.Tensor:
+        """The (3, rows_me, W) send view the next `submit` uses, ordered on the current
+        stream after the gather that last read it."""
+        slot = self.slots[self.next_slot]
+        if slot["work"] is not None:
+            slot["work"].wait()  # the current stream waits for the previous gather of it
+            slot["work"] = None
+        return self._strip_view(slot["send"], self.rows_me)
 
     def submit(self, strip: torch.Tensor) -> None:
         if strip.shape != (3, self.rows_me, self.W):
             raise ValueError(f"strip shape {tuple(strip.shape)} != (3, {self.rows_me}, {self.W})")
         if len(self.pending) == len(self.slots):
             raise RuntimeError("StripGather: every slot is in flight; call finish() first")
+        buf = self.next_buffer()
         slot = self.slots[self.next_slot]
         self.next_slot = (self.next_slot + 1) % len(self.slots)
-        slot["send"][:, :self.rows_me].copy_(strip)
+        if strip.data_ptr() != buf.data_ptr():
+            buf.copy_(strip)
         parts = list(slot["recv"].unbind(0)) if self.rank == 0 else None
         work = dist.gather(slot["send"], parts, dst=0, group=self.group, async_op=True)
+        slot["work"] = work
         self.pending.append((slot, work))
 
     def finish(self) -> torch.Tensor | None:
@@ -103,8 +123,8 @@ class StripGather:
         if self.rank != 0:
             return None
         recv = slot["recv"]
-        return torch.cat([recv[r, :, :rows] for r, (_, rows) in enumerate(self.layout) if rows],
-                         dim=1)
+        return torch.cat([self._strip_view(recv[r], rows)
+                          for r, (_, rows) in enumerate(self.layout) if rows], dim=1)
 
 
 def render_strips(render_fn, H: int, W: int, world: int, rank: int, group=None):

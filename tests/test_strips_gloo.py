@@ -60,7 +60,7 @@ def test_gather_strips_reassembles_frame(tmp_path, oracle_mod, world, H, W):
     np.testing.assert_array_equal(out.view(np.uint32), frame.view(np.uint32))
 
 
-def _stream_worker(rank, world, port, H, W, result_path):
+def _stream_worker(rank, world, port, H, W, result_path, in_place=False):
     from gaussiansplattingviewer_amd.strips import StripGather
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -73,7 +73,12 @@ def _stream_worker(rank, world, port, H, W, result_path):
         sg = StripGather(H, W, world, rank, depth=2)
         got = []
         for k, f in enumerate(frames):  # pipelined: frame k's gather overlaps frame k+1
-            sg.submit(f[:, y0:y0 + rows].clone())
+            if in_place:  # render straight into the send buffer (the bench's path)
+                buf = sg.next_buffer()
+                buf.copy_(f[:, y0:y0 + rows])
+                sg.submit(buf)
+            else:
+                sg.submit(f[:, y0:y0 + rows].clone())
             if k >= 1:
                 got.append(sg.finish())
         got.append(sg.finish())
@@ -85,12 +90,14 @@ def _stream_worker(rank, world, port, H, W, result_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,H,W", [(2, 100, 48), (3, 100, 48)])
-def test_strip_gather_pipelined_stream(tmp_path, world, H, W):
+@pytest.mark.parametrize("world,H,W,in_place", [(2, 100, 48, False), (3, 100, 48, False),
+                                                (3, 100, 48, True), (2, 36, 40, True)])
+def test_strip_gather_pipelined_stream(tmp_path, world, H, W, in_place):
     """StripGather (the bench's pipelined gather): 5 frames, two in flight, reassembled in
-    order and bit-exact on rank 0."""
+    order and bit-exact on rank 0; strips copied in or rendered into the send buffers."""
     rp = tmp_path / "out.npy"
-    mp.start_processes(_stream_worker, args=(world, _free_port(), H, W, str(rp)), nprocs=world,
+    mp.start_processes(_stream_worker, args=(world, _free_port(), H, W, str(rp), in_place),
+                       nprocs=world,
                        join=True, start_method="spawn")
     out = np.load(rp)
     want = np.stack([np.arange(3 * H * W, dtype=np.float32).reshape(3, H, W) * (k + 1)
