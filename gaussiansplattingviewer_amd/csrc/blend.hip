@@ -61,8 +61,10 @@ __device__ __forceinline__ bool may_touch(float x, float y, float A, float B, fl
     if (fmaxf(fmaxf(ulo, -uhi), 0.0f) > ex || fmaxf(fmaxf(vlo, -vhi), 0.0f) > ey) return false;
     if (ulo <= 0.0f && uhi >= 0.0f && vlo <= 0.0f && vhi >= 0.0f) return true;
     // centre outside the box: q is convex, so its minimum over the box lies on an edge, where
-    // it is the 1-D minimum clamped to the edge
-    const float su = -B / C, sv = -B / A;
+    // it is the 1-D minimum clamped to the edge.  The minimiser's slope -B/C (-B/A) comes from
+    // v_rcp_f32 (1 ulp) instead of an IEEE division (~10 VALU): a minimiser a few ulp off
+    // raises q there by C * dv^2 ~ 1e-13 * q, far inside q_lower's 16-ulp rounding margin.
+    const float su = -B * __builtin_amdgcn_rcpf(C), sv = -B * __builtin_amdgcn_rcpf(A);
     float lb = q_lower(A, B, C, ulo, fminf(fmaxf(su * ulo, vlo), vhi));
     lb = fminf(lb, q_lower(A, B, C, uhi, fminf(fmaxf(su * uhi, vlo), vhi)));
     lb = fminf(lb, q_lower(A, B, C, fminf(fmaxf(sv * vlo, ulo), uhi), vlo));
@@ -124,8 +126,8 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
             const float alpha = fminf(0.99f, sp.q.y * __builtin_amdgcn_exp2f(p2));
             vis = !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
             // same arithmetic as k_blend_q (short loop-carried chain through T)
-            const float om = vis ? 1.0f - alpha : 1.0f;
-            test_T = T * om;
+            const float alpha_eff = vis ? alpha : 0.0f;
+            test_T = __builtin_fmaf(-T, alpha_eff, T);
             const bool lo = test_T < 0.0001f;
             wgt = lo ? 0.0f : T - test_T;
             C0 = __builtin_fmaf(sp.q.z, wgt, C0);
@@ -282,7 +284,9 @@ __device__ __forceinline__ uint32_t xcd_work(uint32_t b, uint32_t group) {
 // composited, their ids one chunk earlier still.  Blocks are mapped XCD-aware (xcd_work).
 // kLean: no record prefetch (only the next chunk's ids), so the kernel fits 64 VGPRs and
 // 8 waves per SIMD; the record gathers' latency is then left to the other waves.
-template <bool kFast, bool kLean = false>
+// kContrib: track the last contributor (the n_contrib output); off (no n_contrib requested),
+// the composite step loses one v_cndmask.
+template <bool kFast, bool kLean = false, bool kContrib = true>
 __global__ __launch_bounds__(64, kLean ? 8 : 1) void k_blend_q(const GsrBlendArgs a,
                                                              uint32_t n_work, uint32_t per_xcd) {
     __shared__ StagedSplat s_spl[64];
@@ -318,14 +322,16 @@ __global__ __launch_bounds__(64, kLean ? 8 : 1) void k_blend_q(const GsrBlendArg
                 __builtin_fmaf(dx, __builtin_fmaf(sp.g.z, dx, sp.g.w * dy), sp.q.x * dy * dy);
             const float alpha = fminf(0.99f, sp.q.y * __builtin_amdgcn_exp2f(p2));
             vis = !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
-            const float om = vis ? 1.0f - alpha : 1.0f;
-            test_T = T * om;
+            // T (1 - alpha) as one fma, T - alpha T; alpha_eff = 0 leaves T exactly
+            const float alpha_eff = vis ? alpha : 0.0f;
+            test_T = __builtin_fmaf(-T, alpha_eff, T);
             const bool lo = test_T < 0.0001f;
             const float wgt = lo ? 0.0f : T - test_T;
             C0 = __builtin_fmaf(sp.q.z, wgt, C0);
             C1 = __builtin_fmaf(sp.q.w, wgt, C1);
             C2 = __builtin_fmaf(sp.e.x, wgt, C2);
-            last_contributor = (vis && !lo) ? __float_as_uint(sp.e.y) : last_contributor;
+            if (kContrib)
+                last_contributor = (vis && !lo) ? __float_as_uint(sp.e.y) : last_contributor;
             T = lo ? -fabsf(T) : test_T;
             return;
         } else {
@@ -341,7 +347,7 @@ __global__ __launch_bounds__(64, kLean ? 8 : 1) void k_blend_q(const GsrBlendArg
             C2 = acc ? C2 + sp.e.x * alpha * T : C2;
         }
         T = acc ? test_T : (term ? -fabsf(T) : T);
-        last_contributor = acc ? __float_as_uint(sp.e.y) : last_contributor;
+        if (kContrib) last_contributor = acc ? __float_as_uint(sp.e.y) : last_contributor;
     };
     const float X0 = (float)qx0, Y0 = (float)qy0;
 
@@ -422,7 +428,7 @@ __global__ __launch_bounds__(64, kLean ? 8 : 1) void k_blend_q(const GsrBlendArg
         const size_t plane = (size_t)a.rows_out * a.W;
         const float Tf = fabsf(T);
         if (a.final_T) a.final_T[pid] = Tf;
-        if (a.n_contrib) a.n_contrib[pid] = last_contributor;
+        if (kContrib && a.n_contrib) a.n_contrib[pid] = last_contributor;
         a.out_color[pid] = C0 + Tf * a.bg[0];
         a.out_color[plane + pid] = C1 + Tf * a.bg[1];
         a.out_color[2 * plane + pid] = C2 + Tf * a.bg[2];
@@ -734,7 +740,10 @@ hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s) {
         // grid: whole groups on every XCD (blocks past n_work exit)
         const uint32_t g = a.xcd_group ? a.xcd_group * 8u : 8u;
         const uint32_t per_xcd = (n_work + g - 1) / g * g / 8u;
-        if (a.fast && a.lean)
+        if (a.fast && a.lean && !a.n_contrib)
+            hipLaunchKernelGGL((k_blend_q<true, true, false>), dim3(8u * per_xcd), dim3(64), 0, s,
+                               a, n_work, per_xcd);
+        else if (a.fast && a.lean)
             hipLaunchKernelGGL((k_blend_q<true, true>), dim3(8u * per_xcd), dim3(64), 0, s, a,
                                n_work, per_xcd);
         else if (a.fast)

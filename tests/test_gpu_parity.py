@@ -225,34 +225,73 @@ def test_headline_config_c3(gpu, c3_oracle, fast):
     assert_parity(hip, orc)
 
 
-VARIANTS = {  # option, alternative value, default
-    "onesweep": (_lib.GSR_OPT_SORT_ONESWEEP, 1, 0),
-    "unfused": (_lib.GSR_OPT_FUSED_BINNING, 0, 1),
-    "tile_shape0": (_lib.GSR_OPT_TILE_SORT_SHAPE, 0, 3),
-    "tile_shape5": (_lib.GSR_OPT_TILE_SORT_SHAPE, 5, 3),
-    "depth_shape0": (_lib.GSR_OPT_DEPTH_SORT_SHAPE, 0, 3),
-    "depth_shape5": (_lib.GSR_OPT_DEPTH_SORT_SHAPE, 5, 3),
-    "blend_blocks": (_lib.GSR_OPT_BLEND_WAVE_QUADRANTS, 0, 1),
-    "inline_color": (_lib.GSR_OPT_SPLIT_COLOR, 0, 1),
+VARIANTS = {  # [(option, alternative value, default), ...]
+    "onesweep": [(_lib.GSR_OPT_SORT_ONESWEEP, 1, 0)],
+    "unfused": [(_lib.GSR_OPT_FUSED_BINNING, 0, 1)],
+    "tile_shape0": [(_lib.GSR_OPT_TILE_SORT_SHAPE, 0, 3)],
+    "tile_shape5": [(_lib.GSR_OPT_TILE_SORT_SHAPE, 5, 3)],
+    "depth_shape0": [(_lib.GSR_OPT_DEPTH_SORT_SHAPE, 0, 3)],
+    "depth_shape5": [(_lib.GSR_OPT_DEPTH_SORT_SHAPE, 5, 3)],
+    "blend_blocks": [(_lib.GSR_OPT_BLEND_WAVE_QUADRANTS, 0, 1)],
+    "inline_color": [(_lib.GSR_OPT_SPLIT_COLOR, 0, 1)],
+    "inline_color_onesweep": [(_lib.GSR_OPT_SPLIT_COLOR, 0, 1), (_lib.GSR_OPT_SORT_ONESWEEP, 1, 0)],
 }
+
+
+class _options:
+    """Set a VARIANTS entry's options for the duration of a with-block."""
+
+    def __init__(self, gpu, opts):
+        self.gpu, self.opts = gpu, opts
+
+    def __enter__(self):
+        for opt, val, _ in self.opts:
+            _set_option(self.gpu, opt, val)
+
+    def __exit__(self, *exc):
+        for opt, _, default in self.opts:
+            _set_option(self.gpu, opt, default)
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
 @pytest.mark.parametrize("size", [(1920, 1080), (16, 16), (4200, 64)])
 def test_sort_implementations_agree(gpu, variant, size):
     """The defaults (duplicate fused with the first reduce-then-scan pass, 8x8 sort tiles, one
-    wave per blend quadrant) and the alternatives -- onesweep sort, separate duplicate
-    kernel, other sort tile shapes, 4-wave blend blocks -- give identical binning and images.  Sizes: 1 tile (tbits = 0) and > 8 bits of tile id in x."""
+    wave per blend quadrant, colour on the second stream) and the alternatives -- onesweep
+    sort, separate duplicate kernel, other sort tile shapes, 4-wave blend blocks, inline
+    colour -- give identical binning and images.  Sizes: 1 tile (tbits = 0) and > 8 bits of
+    tile id in x."""
     w, h = size
     P = 300_000 if w * h > 10_000 else 20_000
     s = scene_inputs(synthetic_gaussians(P, 3, 21), static_camera(w, h, (0.5, 0.2, 3.5)), 3)
     ref = run_hip(s, gpu)
-    opt, val, default = VARIANTS[variant]
-    _set_option(gpu, opt, val)
-    try:
+    with _options(gpu, VARIANTS[variant]):
         alt = run_hip(s, gpu)
-    finally:
-        _set_option(gpu, opt, default)
     assert ref["num_rendered"] > 0
     for k in ("point_list", "point_tiles", "ranges", "color", "n_contrib"):
         np.testing.assert_array_equal(alt[k], ref[k], err_msg=k)
+
+
+@pytest.mark.parametrize("variant", ["default", "onesweep", "unfused"])
+def test_long_tile_lists_and_depth_ties(gpu, oracle_mod, variant):
+    """Tiles covered by more than 2048 splats (multi-chunk digit runs in the tile sort, long
+    blend lists) and half of the Gaussians at one depth (ties: upstream orders them by
+    Gaussian index, so the stable depth sort must keep index order)."""
+    g = synthetic_gaussians(15000, 3, 23)
+    g.scale[:] = np.float32(0.3)
+    g.xyz[:7000, 2] = np.float32(0.25)  # one depth for half of them
+    s = scene_inputs(g, static_camera(320, 240, (0, 0, 3.0)), 3)
+    orc = run_oracle(oracle_mod, s)
+    counts = orc["ranges"][:, 1] - orc["ranges"][:, 0]
+    assert counts.max() > 2048 and (counts > 2048).sum() > 10, counts.max()
+    with _options(gpu, VARIANTS.get(variant, [])):
+        hip = run_hip(s, gpu)
+    assert_parity(hip, orc)
+
+
+def test_tile_lists_of_one_depth(gpu, oracle_mod):
+    """Every Gaussian at the same depth: each tile's list is already in upstream's order."""
+    g = synthetic_gaussians(3000, 3, 24)
+    g.xyz[:, 2] = np.float32(-0.5)
+    s = scene_inputs(g, static_camera(160, 120, (0, 0, 3.0)), 1)
+    assert_parity(run_hip(s, gpu), run_oracle(oracle_mod, s))
