@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgsr.so")
+# GSR_LIB: another build of the library (A/B tuning builds); default the in-tree libgsr.so
+LIB_PATH = os.environ.get("GSR_LIB") or os.path.join(_HERE, "libgsr.so")
 ABI_VERSION = 1
 
 GSR_OPT_BLEND_CULL = 1
@@ -22,6 +23,7 @@ GSR_OPT_FUSED_BINNING = 5
 GSR_OPT_BLEND_WAVE_QUADRANTS = 6
 GSR_OPT_DEPTH_SORT_SHAPE = 7
 GSR_OPT_SPLIT_COLOR = 8
+GSR_OPT_PACKED_PAIRS = 9
 
 # Symbols include/gsr.h declares (checked by the CPU test suite).
 EXPORTED_SYMBOLS = (

@@ -62,6 +62,8 @@ struct gsr_context {
     int64_t last_K = 0;
     uint32_t last_gx = 0, last_gy = 0, last_rb = 0, last_re = 0;
     uint32_t *last_point_list = nullptr, *last_tiles_local = nullptr;
+    bool last_packed = false;             // last_point_list is a packed pair list (no keys)
+    uint32_t last_id_mask = 0xFFFFFFFFu;  // packed word -> Gaussian id
     // options / timing
     int cull = 1;
     int fast = 1;
@@ -74,6 +76,10 @@ struct gsr_context {
     // sort and the frame is ~2% slower; 0 = k_ranges on the main stream).  env GSR_AUX_RANGES
     int aux_ranges = 2;
     int blend_wave_quadrants = 1;
+    // GSR_OPT_PACKED_PAIRS: one 32-bit word per (tile, Gaussian) pair -- the tile-id bits the
+    // second tile-sort pass needs above the Gaussian id -- instead of a key and a value array
+    // (needs the second-stream ranges; falls back when the bits do not fit)
+    int packed_pairs = 1;
     int color_blocks = 512;    // grid cap of the overlapped colour pass
     uint32_t blend_xcd_group = 16;  // tuning (env GSR_BLEND_XCD_GROUP)
     int blend_lean = 1;             // tuning (env GSR_BLEND_LEAN=0: record prefetch, 7 waves)
@@ -230,6 +236,8 @@ int gsr_create(gsr_context **out) {
     if (env_cb) ctx->color_blocks = std::atoi(env_cb);
     const char *env_ln = std::getenv("GSR_BLEND_LEAN");
     if (env_ln) ctx->blend_lean = std::atoi(env_ln);
+    const char *env_pp = std::getenv("GSR_PACKED_PAIRS");
+    if (env_pp) ctx->packed_pairs = std::atoi(env_pp);
     const char *env_ar = std::getenv("GSR_AUX_RANGES");
     if (env_ar) ctx->aux_ranges = std::atoi(env_ar);
     const char *env_xg = std::getenv("GSR_BLEND_XCD_GROUP");
@@ -343,6 +351,10 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
     if (option == GSR_OPT_DEPTH_SORT_SHAPE) {
         if (value < 0 || value > 5) return fail(GSR_E_INVALID, "gsr_set_option: shape 0..5");
         ctx->depth_sort_shape = (int)value;
+        return GSR_OK;
+    }
+    if (option == GSR_OPT_PACKED_PAIRS) {
+        ctx->packed_pairs = value ? 1 : 0;
         return GSR_OK;
     }
     if (option == GSR_OPT_TILE_SORT_SHAPE) {
@@ -471,6 +483,8 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         ctx->last_K = 0;
         ctx->last_gx = gx; ctx->last_gy = gy; ctx->last_rb = rb; ctx->last_re = re;
         ctx->last_point_list = static_cast<uint32_t *>(ctx->tile_vals.p);
+        ctx->last_id_mask = 0xFFFFFFFFu;
+        ctx->last_packed = false;
         ctx->last_tiles_local = static_cast<uint32_t *>(ctx->tile_keys.p);
         ctx->have_forward = true;
         return GSR_OK;
@@ -638,6 +652,13 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     hist = static_cast<uint32_t *>(ctx->hist.p);  // may have been regrown
     const GsrRadixPlan tplan = gsr_radix_plan(0, tbits);
     const bool fused = !ctx->onesweep && ctx->fused_binning;
+    // packed pair list: word = (tile id >> first-pass bits) << pack_shift | Gaussian id; the
+    // pair keys are not stored (the ranges come from the second stream)
+    const int high_bits = tplan.n == 2 ? tplan.nbits[1] : 0;
+    const int pack_shift = 32 - high_bits;
+    const bool packed = ctx->packed_pairs && fused && aux_ranges && tplan.n <= 2 &&
+                        (pack_shift == 32 || (uint64_t)P <= (1ull << pack_shift));
+    const uint32_t id_mask = (packed && pack_shift < 32) ? (1u << pack_shift) - 1u : 0xFFFFFFFFu;
     if (K > 0) {
         GSR_HIP(gsr_launch_scan_down(perm, rect_sorted, partials, P, d_valid, d_total, bin,
                                      chunk_first, s),
@@ -649,7 +670,8 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
                                              tplan.n ? tplan.nbits[0] : 0, hist, digit_total,
                                              tk_alt, tv_alt,
                                              static_cast<uint2 *>(ctx->ranges_local.p),
-                                             aux_ranges ? 0u : (uint32_t)T_strip, s),
+                                             aux_ranges ? 0u : (uint32_t)T_strip, s,
+                                             packed ? pack_shift : -1),
                     "duplicate launch");
             std::swap(tk, tk_alt);
             std::swap(tv, tv_alt);
@@ -668,6 +690,13 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         GSR_HIP(gsr_onesweep_sort(&tk, &tv, &tk_alt, &tv_alt, (int64_t)K, 0, tbits,
                                   K > 0 ? GSR_HIST_READY : GSR_HIST_COUNT, onesweep_ws(ctx, 1), s),
                 "tile sort launch");
+    } else if (packed) {  // the remaining tile bits of the packed words, keys only
+        uint32_t *no_vals = nullptr, *no_vals_alt = nullptr;
+        if (high_bits > 0)
+            GSR_HIP(gsr_radix_sort_pairs(&tv, &no_vals, &tv_alt, &no_vals_alt, (int64_t)K,
+                                         pack_shift, 32, hist, digit_total, s,
+                                         ctx->tile_sort_shape, 0),
+                    "tile sort launch");
     } else {
         GSR_HIP(gsr_radix_sort_pairs(&tk, &tv, &tk_alt, &tv_alt, (int64_t)K, 0, tbits, hist,
                                      digit_total, s, ctx->tile_sort_shape, fused ? 1 : 0),
@@ -710,6 +739,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     ba.wave_quadrants = ctx->blend_wave_quadrants;
     ba.xcd_group = ctx->blend_xcd_group;
     ba.lean = ctx->blend_lean;
+    ba.id_mask = id_mask;
     ba.stamps = ctx->blend_stamps;
     GSR_HIP(gsr_launch_blend(ba, s), "blend launch");
     GSR_TRY(stage_end(6));
@@ -719,6 +749,8 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     ctx->last_gx = gx; ctx->last_gy = gy; ctx->last_rb = rb; ctx->last_re = re;
     ctx->last_point_list = tv;
     ctx->last_tiles_local = tk;
+    ctx->last_id_mask = id_mask;
+    ctx->last_packed = packed && K > 0;
 
     ctx->have_forward = true;
     if (tmode) ++ctx->timed_frames;
@@ -736,13 +768,27 @@ int gsr_get_binning(gsr_context *ctx, uint32_t *point_list, uint32_t *point_tile
     const uint64_t T_strip = (uint64_t)ctx->last_gx * (ctx->last_re - ctx->last_rb);
     if (num_rendered) *num_rendered = K;
     if (num_tiles) *num_tiles = (int32_t)T;
-    if (point_list && K > 0)
-        GSR_HIP(hipMemcpyAsync(point_list, ctx->last_point_list, (size_t)K * 4,
-                               hipMemcpyDeviceToDevice, s),
-                "hipMemcpyAsync(point_list)");
-    if (point_tiles)
-        GSR_HIP(gsr_launch_globalize_tiles(ctx->last_tiles_local, K, (uint32_t)off, point_tiles, s),
-                "globalize launch");
+    if (point_list && K > 0) {
+        if (ctx->last_id_mask != 0xFFFFFFFFu)
+            GSR_HIP(gsr_launch_unpack_ids(ctx->last_point_list, K, ctx->last_id_mask, point_list,
+                                          s),
+                    "unpack launch");
+        else
+            GSR_HIP(hipMemcpyAsync(point_list, ctx->last_point_list, (size_t)K * 4,
+                                   hipMemcpyDeviceToDevice, s),
+                    "hipMemcpyAsync(point_list)");
+    }
+    if (point_tiles && K > 0) {
+        if (!ctx->last_packed)
+            GSR_HIP(gsr_launch_globalize_tiles(ctx->last_tiles_local, K, (uint32_t)off,
+                                               point_tiles, s),
+                    "globalize launch");
+        else  // packed list (no key array): the tile of every pair from the ranges
+            GSR_HIP(gsr_launch_fill_tiles(static_cast<const uint2 *>(ctx->ranges_local.p),
+                                          (uint32_t)T_strip, (uint32_t)off, point_tiles, s),
+                    "fill_tiles launch");
+    }
+
     if (ranges) {
         GSR_HIP(hipMemsetAsync(ranges, 0, T * 8, s), "hipMemsetAsync(ranges)");
         GSR_HIP(hipMemcpyAsync(reinterpret_cast<char *>(ranges) + off * 8, ctx->ranges_local.p,

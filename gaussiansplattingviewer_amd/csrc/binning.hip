@@ -328,7 +328,7 @@ __global__ __launch_bounds__(kFW * 64) void k_dup_scatter(
     const uint4 *__restrict__ bin, const uint32_t *__restrict__ chunk_first, uint32_t K,
     uint32_t n_chunks, uint32_t gx, int shift, int nbits, const uint32_t *__restrict__ hist,
     int64_t nb, const uint32_t *__restrict__ digit_total, uint32_t *__restrict__ keys_out,
-    uint32_t *__restrict__ vals_out) {
+    uint32_t *__restrict__ vals_out, int pack_shift) {
     union alignas(16) Smem {
         DupStage st;
         struct {
@@ -363,9 +363,17 @@ __global__ __launch_bounds__(kFW * 64) void k_dup_scatter(
         kk[j] = u.kv.keys[e];
         vv[j] = u.kv.vals[e];
     }
+    // packed pair list (pack_shift >= 0): one word per pair, the tile id bits the later
+    // passes sort on (above this pass's digit) over the Gaussian id; no key array is written
+    if (pack_shift >= 0) {
+#pragma unroll
+        for (int j = 0; j < kFIt; ++j)
+            vv[j] |= pack_shift < 32 ? (kk[j] >> (shift + nbits)) << pack_shift : 0u;
+    }
     // (radix_tile_scatter's first barrier orders these reads before its LDS writes)
     radix_tile_scatter<kFW, kFIt>(kk, vv, (int)(o_end - c * kFChunk), shift, nbits, hist, nb, c,
-                                  digit_total, keys_out, vals_out, sm, u.kv.keys, u.kv.vals);
+                                  digit_total, pack_shift >= 0 ? nullptr : keys_out, vals_out,
+                                  sm, u.kv.keys, u.kv.vals);
 }
 
 // upstream identifyTileRanges over the tile-sorted keys (ranges pre-zeroed).
@@ -400,6 +408,23 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const uint32_t *__restrict__ 
         if (i == K - 1) ranges[2 * cur + 1] = (uint32_t)K;
         prev = cur;
     }
+}
+
+// Packed pair list -> Gaussian ids (gsr_get_binning).
+__global__ __launch_bounds__(kBlock) void k_unpack_ids(const uint32_t *__restrict__ packed,
+                                                       int64_t K, uint32_t mask,
+                                                       uint32_t *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < K) out[i] = packed[i] & mask;
+}
+
+// Tile id of every pair from the tile ranges (gsr_get_binning with a packed list): block t
+// fills its tile's range with offset + t.
+__global__ __launch_bounds__(kBlock) void k_fill_tiles(const uint2 *__restrict__ ranges,
+                                                       uint32_t offset,
+                                                       uint32_t *__restrict__ out) {
+    const uint2 r = ranges[blockIdx.x];
+    for (uint32_t i = r.x + threadIdx.x; i < r.y; i += kBlock) out[i] = offset + blockIdx.x;
 }
 
 __global__ __launch_bounds__(kBlock) void k_globalize(const uint32_t *__restrict__ local, int64_t K,
@@ -456,7 +481,8 @@ int64_t gsr_fused_chunks(int64_t K) { return (K + kFChunk - 1) / kFChunk; }
 hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_first, int64_t K,
                                     uint32_t gx, int shift, int nbits, uint32_t *hist,
                                     uint32_t *digit_total, uint32_t *keys_out, uint32_t *vals_out,
-                                    uint2 *ranges_zero, uint32_t n_ranges, hipStream_t s) {
+                                    uint2 *ranges_zero, uint32_t n_ranges, hipStream_t s,
+                                    int pack_shift) {
     const int64_t nb = gsr_fused_chunks(K);
     if (nb == 0) return hipSuccess;
     const uint32_t nc = (uint32_t)gsr_duplicate_chunks(K);
@@ -467,7 +493,7 @@ hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_firs
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_dup_scatter, dim3((unsigned)nb), dim3(kFW * 64), 0, s, bin, chunk_first,
                        (uint32_t)K, nc, gx, shift, nbits, hist, nb, digit_total, keys_out,
-                       vals_out);
+                       vals_out, pack_shift);
     return hipGetLastError();
 }
 
@@ -602,5 +628,20 @@ hipError_t gsr_launch_globalize_tiles(const uint32_t *local, int64_t K, uint32_t
     if (K == 0) return hipSuccess;
     hipLaunchKernelGGL(k_globalize, dim3((unsigned)((K + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        s, local, K, offset, global);
+    return hipGetLastError();
+}
+
+hipError_t gsr_launch_unpack_ids(const uint32_t *packed, int64_t K, uint32_t mask, uint32_t *out,
+                                 hipStream_t s) {
+    if (K <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unpack_ids, dim3((unsigned)((K + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       s, packed, K, mask, out);
+    return hipGetLastError();
+}
+
+hipError_t gsr_launch_fill_tiles(const uint2 *ranges, uint32_t n_tiles, uint32_t offset,
+                                 uint32_t *out, hipStream_t s) {
+    if (n_tiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fill_tiles, dim3(n_tiles), dim3(kBlock), 0, s, ranges, offset, out);
     return hipGetLastError();
 }

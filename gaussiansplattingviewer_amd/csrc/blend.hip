@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void k_blend(const GsrBlendArgs a) {
         if (__syncthreads_count(T <= 0.0f) == 256) break;
         const uint32_t idx = start + tid;
         if (idx < range.y) {
-            const SplatRecord r = a.records[a.point_list[idx]];
+            const SplatRecord r = a.records[(a.point_list[idx] & a.id_mask)];
             uint32_t m = 0xF;
             if (a.cull) {
                 const float x = r.a.x, y = r.a.y, A = r.a.z, B = r.a.w, C = r.b.x;
@@ -353,11 +353,11 @@ __global__ __launch_bounds__(64, kLean ? 8 : 1) void k_blend_q(const GsrBlendArg
 
     // pipeline: records of chunk c+1 and ids of chunk c+2 are in flight while c composites
     uint32_t i0 = range.x + (uint32_t)lane;
-    uint32_t id_next = i0 < range.y ? a.point_list[i0] : 0u;
+    uint32_t id_next = i0 < range.y ? (a.point_list[i0] & a.id_mask) : 0u;
     SplatRecord r_next;
     if (!kLean) {
         if (i0 < range.y) r_next = a.records[id_next];
-        id_next = i0 + 64u < range.y ? a.point_list[i0 + 64u] : 0u;
+        id_next = i0 + 64u < range.y ? (a.point_list[i0 + 64u] & a.id_mask) : 0u;
     }
     for (uint32_t start = range.x; start < range.y; start += 64) {
         const uint32_t idx = start + (uint32_t)lane;
@@ -365,11 +365,11 @@ __global__ __launch_bounds__(64, kLean ? 8 : 1) void k_blend_q(const GsrBlendArg
         SplatRecord r;
         if (kLean) {
             if (valid) r = a.records[id_next];
-            if (idx + 64u < range.y) id_next = a.point_list[idx + 64u];
+            if (idx + 64u < range.y) id_next = (a.point_list[idx + 64u] & a.id_mask);
         } else {
             r = r_next;
             if (idx + 64u < range.y) r_next = a.records[id_next];
-            if (idx + 128u < range.y) id_next = a.point_list[idx + 128u];
+            if (idx + 128u < range.y) id_next = (a.point_list[idx + 128u] & a.id_mask);
         }
 
         bool keep = valid;
@@ -505,15 +505,15 @@ __global__ __launch_bounds__(64) void k_blend_h(const GsrBlendArgs a, uint32_t n
     const float kL2e = 1.4426950408889634f;
 
     uint32_t i0 = range.x + (uint32_t)lane;
-    uint32_t id_next = i0 + 64u < range.y ? a.point_list[i0 + 64u] : 0u;
+    uint32_t id_next = i0 + 64u < range.y ? (a.point_list[i0 + 64u] & a.id_mask) : 0u;
     SplatRecord r_next;
-    if (i0 < range.y) r_next = a.records[a.point_list[i0]];
+    if (i0 < range.y) r_next = a.records[(a.point_list[i0] & a.id_mask)];
     for (uint32_t start = range.x; start < range.y; start += 64) {
         const uint32_t idx = start + (uint32_t)lane;
         const bool valid = idx < range.y;
         const SplatRecord r = r_next;
         if (idx + 64u < range.y) r_next = a.records[id_next];
-        if (idx + 128u < range.y) id_next = a.point_list[idx + 128u];
+        if (idx + 128u < range.y) id_next = (a.point_list[idx + 128u] & a.id_mask);
 
         bool keep = valid;
         if (valid && a.cull)
@@ -645,7 +645,7 @@ __global__ __launch_bounds__(128) void k_blend_fast2(const GsrBlendArgs a) {
         for (int t = tid; t < kBatch; t += 128) {
             const uint32_t idx = start + t;
             if (idx >= range.y) break;
-            const SplatRecord r = a.records[a.point_list[idx]];
+            const SplatRecord r = a.records[(a.point_list[idx] & a.id_mask)];
             uint32_t m = 0xF;
             if (a.cull) {
                 const float x = r.a.x, y = r.a.y, A = r.a.z, B = r.a.w, C = r.b.x;

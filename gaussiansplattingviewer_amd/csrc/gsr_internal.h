@@ -303,7 +303,14 @@ int64_t gsr_fused_chunks(int64_t K);
 hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_first, int64_t K,
                                     uint32_t gx, int shift, int nbits, uint32_t *hist,
                                     uint32_t *digit_total, uint32_t *keys_out, uint32_t *vals_out,
-                                    uint2 *ranges_zero, uint32_t n_ranges, hipStream_t s);
+                                    uint2 *ranges_zero, uint32_t n_ranges, hipStream_t s,
+                                    int pack_shift = -1);
+// Packed pair lists (gsr_launch_dup_sort_pass with pack_shift >= 0): ids = packed & mask;
+// tile ids (offset + strip-local tile) from the tile ranges.
+hipError_t gsr_launch_unpack_ids(const uint32_t *packed, int64_t K, uint32_t mask, uint32_t *out,
+                                 hipStream_t s);
+hipError_t gsr_launch_fill_tiles(const uint2 *ranges, uint32_t n_tiles, uint32_t offset,
+                                 uint32_t *out, hipStream_t s);
 hipError_t gsr_launch_ranges(const uint32_t *tile_keys, int64_t K, uint32_t *ranges,
                              hipStream_t s);
 // Tile ranges from the Gaussians' strip tile rects alone (no sorted keys): per-tile pair
@@ -334,6 +341,7 @@ struct GsrBlendArgs {
     int wave_quadrants;  // 1: one independent wave per (tile, quadrant) (k_blend_q)
     uint32_t xcd_group;  // work items per XCD round-robin group (0: plain block order)
     int lean;            // fast mode: k_blend_q<true, true> (no record prefetch, 8 waves/SIMD)
+    uint32_t id_mask;    // point_list word -> Gaussian id (packed pair lists; else ~0u)
     // diagnostics (env GSR_DEBUG_BLEND_STAMPS): per-phase s_memtime sums, see blend.hip
     unsigned long long *stamps;
 };

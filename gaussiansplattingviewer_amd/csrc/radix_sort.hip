@@ -165,7 +165,7 @@ __global__ __launch_bounds__(kW * 64) void k_rs_downsweep(
         const int64_t e = base + w * (kT / kW) + j * 64 + lane;
         const bool valid = e < n;
         k[j] = valid ? keys_in[e] : 0xFFFFFFFFu;  // tail -> largest digit, after every real key
-        v[j] = valid ? vals_in[e] : 0u;
+        v[j] = (valid && vals_in) ? vals_in[e] : 0u;  // vals_in == nullptr: keys only
     }
     const int64_t rem = n - base;
     radix_tile_scatter<kW, kIt, kDrop>(k, v, rem < kT ? (int)rem : kT, shift, nbits, hist, nb,
@@ -428,7 +428,7 @@ static void rts_sort(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt, uint
                               digit_total + kRadix * p, s);
         }
         std::swap(*keys, *keys_alt);
-        std::swap(*vals, *vals_alt);
+        std::swap(*vals, *vals_alt);  // (keys-only sorts pass pointers to null pointers)
     }
 }
 

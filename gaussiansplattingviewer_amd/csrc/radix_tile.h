@@ -48,6 +48,8 @@ struct RadixTileSmem {
 // upsweep must not count them either).
 // s_keys / s_vals: kT words each (may alias storage the caller no longer needs: the first
 // write to them follows two block barriers).
+// keys_out == nullptr: only the values are written (the packed pair list, binning.hip);
+// vals_out == nullptr: keys only (v is ignored).
 constexpr uint32_t kDropKey = 0xFFFFFFFFu;
 
 template <int kW, int kIt, bool kDrop = false>
@@ -116,15 +118,15 @@ __device__ __forceinline__ void radix_tile_scatter(
         const uint32_t d = (k[j] >> shift) & mask;
         const uint32_t pos = sm.wcnt[w][d] + rank[j];
         s_keys[pos] = k[j];
-        s_vals[pos] = v[j];
+        if (vals_out) s_vals[pos] = v[j];
     }
     __syncthreads();
     const int n_out = kDrop ? (int)sm.tmp[2 * kW] : valid;  // kept elements of the tile
     for (int i = tid; i < n_out; i += kThreads) {
         const uint32_t kk = s_keys[i];
         const uint32_t g = sm.delta[(kk >> shift) & mask] + (uint32_t)i;
-        keys_out[g] = kk;
-        vals_out[g] = s_vals[i];
+        if (keys_out) keys_out[g] = kk;
+        if (vals_out) vals_out[g] = s_vals[i];
     }
 }
 

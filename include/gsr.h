@@ -210,9 +210,14 @@ const char *gsr_stage_name(int i);
 /*   GSR_OPT_SPLIT_COLOR (default 1): SH -> RGB runs as its own kernel on an internal second
  *     stream, overlapped with the depth sort and the binning; 0 = inside the preprocess
  *     kernel.  Identical results. */
+/*   GSR_OPT_PACKED_PAIRS (default 1): the (tile, Gaussian) pair list is one 32-bit word per
+ *     pair -- the tile-id bits the second tile-sort pass needs above the Gaussian id --
+ *     written once by the fused duplicate and sorted keys-only; used when the tile ranges come
+ *     from the second stream and the bits fit (P <= 2^(32 - second-pass bits)), else key and
+ *     value arrays.  Identical results. */
 enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_SORT_ONESWEEP = 3,
        GSR_OPT_TILE_SORT_SHAPE = 4, GSR_OPT_FUSED_BINNING = 5, GSR_OPT_BLEND_WAVE_QUADRANTS = 6,
-       GSR_OPT_DEPTH_SORT_SHAPE = 7, GSR_OPT_SPLIT_COLOR = 8 };
+       GSR_OPT_DEPTH_SORT_SHAPE = 7, GSR_OPT_SPLIT_COLOR = 8, GSR_OPT_PACKED_PAIRS = 9 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
 
 #ifdef __cplusplus
