@@ -112,7 +112,7 @@ class Scene:
 # tools/profile.sh + tools/prof_summary.py --json) of the default configuration, and the kernel
 # each stage's roofline refers to.  The bench cannot read PMC counters itself; the profile is
 # of this same command (c3, default options).
-TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r01_c3_v8_kernels.json")
+TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r01_c3_v9_kernels.json")
 STAGE_KERNEL = {"blend": "k_blend_q<true", "preprocess": "k_preprocess<false>",
                 "color": "k_color", "depth_sort": None, "duplicate": "k_dup_scatter",
                 "tile_sort": None, "scan": None, "ranges": "k_ranges"}
