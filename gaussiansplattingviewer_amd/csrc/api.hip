@@ -69,7 +69,9 @@ struct gsr_context {
     int fast = 1;
     int onesweep = 0;
     int tile_sort_shape = 3;  // 8 waves x 8 keys/lane: fastest measured
-    int depth_sort_shape = 3;  // 8x8: 78 us vs 89 for 4x16 at 1M keys (bench, round 1)
+    // 4 waves x 4 keys (1024-key tiles): as fast as 8x8 at the full C3 frame (94 vs 92 us) and
+    // faster on strips, whose compacted sorts are small (65 vs 79 us on one of 8 strips)
+    int depth_sort_shape = 5;
     int fused_binning = 1;    // duplicate fused with the first tile-sort pass
     // tile ranges from the rects' per-tile counts on the second stream, after the colour
     // (2; 1 = before it: the colour then overlaps the duplicate stage instead of the depth

@@ -284,7 +284,8 @@ __device__ __forceinline__ void color_one(const GsrPreprocessArgs &a, int64_t id
 // fully coalesced 16-B loads (lane l takes float4 i*64 + l), transposes them through LDS
 // (rows padded to 13 float4 so the per-lane 16-B reads are bank-conflict free) and each lane
 // evaluates its own row; rows of invisible Gaussians are skipped when the whole wave is
-// invisible.  Otherwise every lane reads its own row (color_from_sh).
+// invisible.  Otherwise -- or when fewer than 16 of the wave's 64 Gaussians need a colour --
+// every lane that needs one reads its own row (color_from_sh).
 constexpr int kShRowPad = 13;  // float4 per LDS row
 __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
     __shared__ float4 s_sh[4][64 * kShRowPad];
@@ -297,8 +298,11 @@ __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
         // colour needed: Gaussians with pairs in this strip (the blend reads them), or every
         // visible one when the caller asked for the rgb output (upstream semantics)
         const bool vis = in && (a.rgb ? a.radii[idx] != 0 : a.strip_rect[idx].x != 0u);
-        if (__ballot(vis) == 0ull) continue;
-        if (!a.sh_vec4 || a.colors_precomp || a.D != 3) {
+        const uint64_t vis_mask = __ballot(vis);
+        if (vis_mask == 0ull) continue;
+        // few colours needed in this wave (a strip of a multi-GPU frame): per-lane row reads
+        // move only the needed rows, not the wave's whole 12 KiB
+        if (!a.sh_vec4 || a.colors_precomp || a.D != 3 || __popcll(vis_mask) < 16) {
             if (vis) color_one(a, idx);
             continue;
         }

@@ -200,7 +200,7 @@ const char *gsr_stage_name(int i);
  *     see DESIGN.md). */
 /*   GSR_OPT_TILE_SORT_SHAPE (tuning): tile shape of the pair sort's reduce-then-scan kernels,
  *     0 = 4 waves x 16 keys/lane, 1 = 16x16, 2 = 4x8, 3 = 8x8 (default), 4 = 8x16, 5 = 4x4.
- *     GSR_OPT_DEPTH_SORT_SHAPE: the same for the per-Gaussian depth sort (default 3). */
+ *     GSR_OPT_DEPTH_SORT_SHAPE: the same for the per-Gaussian depth sort (default 5). */
 /*   GSR_OPT_FUSED_BINNING (default 1): the pair duplication regenerates each 4096-pair chunk
  *     and performs the tile sort's first radix pass in the same kernel (reduce-then-scan
  *     sort only); 0 = separate duplicate kernel + full sort.  Identical results. */

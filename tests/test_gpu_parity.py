@@ -231,8 +231,8 @@ VARIANTS = {  # [(option, alternative value, default), ...]
     "unfused": [(_lib.GSR_OPT_FUSED_BINNING, 0, 1)],
     "tile_shape0": [(_lib.GSR_OPT_TILE_SORT_SHAPE, 0, 3)],
     "tile_shape5": [(_lib.GSR_OPT_TILE_SORT_SHAPE, 5, 3)],
-    "depth_shape0": [(_lib.GSR_OPT_DEPTH_SORT_SHAPE, 0, 3)],
-    "depth_shape5": [(_lib.GSR_OPT_DEPTH_SORT_SHAPE, 5, 3)],
+    "depth_shape0": [(_lib.GSR_OPT_DEPTH_SORT_SHAPE, 0, 5)],
+    "depth_shape3": [(_lib.GSR_OPT_DEPTH_SORT_SHAPE, 3, 5)],
     "blend_blocks": [(_lib.GSR_OPT_BLEND_WAVE_QUADRANTS, 0, 1)],
     "inline_color": [(_lib.GSR_OPT_SPLIT_COLOR, 0, 1)],
     "inline_color_onesweep": [(_lib.GSR_OPT_SPLIT_COLOR, 0, 1), (_lib.GSR_OPT_SORT_ONESWEEP, 1, 0)],
