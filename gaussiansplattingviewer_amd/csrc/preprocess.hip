@@ -186,10 +186,15 @@ __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, i
                     strip_rect = make_uint2(rc.x0 | ((rc.x1 - rc.x0) << 16),
                                             (sy0 - a.row_begin) | ((sy1 - sy0) << 16));
                 if (strip_tiles) key = __float_as_uint(p_view.z);  // z > 0.2: bits are monotone
-                const float3 cd = cull_data(conic_a, conic_b, conic_c, opacity);
+                // the blend's record (and its double-precision cull data) only for Gaussians
+                // with pairs in this strip: on a strip of a multi-GPU frame most have none
+                float3 cd = make_float3(0.f, 0.f, 0.f);
                 SplatRecord &rec = a.records[idx];
-                rec.a = make_float4(px, py, conic_a, conic_b);
-                rec.b = make_float4(conic_c, opacity, cd.x, cd.y);
+                if (strip_tiles) {
+                    cd = cull_data(conic_a, conic_b, conic_c, opacity);
+                    rec.a = make_float4(px, py, conic_a, conic_b);
+                    rec.b = make_float4(conic_c, opacity, cd.x, cd.y);
+                }
                 if (kColor) {
                     float3 col;
                     if (a.colors_precomp) {
@@ -204,8 +209,8 @@ __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, i
                             a.rgb[3 * idx + 2] = col.z;
                         }
                     }
-                    rec.c = make_float4(cd.z, col.x, col.y, col.z);
-                } else {
+                    if (strip_tiles) rec.c = make_float4(cd.z, col.x, col.y, col.z);
+                } else if (strip_tiles) {
                     rec.c.x = cd.z;  // c.yzw: colour, written by k_color
                 }
                 if (a.depths) a.depths[idx] = p_view.z;
