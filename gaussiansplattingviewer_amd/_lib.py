@@ -24,6 +24,7 @@ GSR_OPT_BLEND_WAVE_QUADRANTS = 6
 GSR_OPT_DEPTH_SORT_SHAPE = 7
 GSR_OPT_SPLIT_COLOR = 8
 GSR_OPT_PACKED_PAIRS = 9
+GSR_OPT_COLUMN_PAIRS = 10
 
 # Symbols include/gsr.h declares (checked by the CPU test suite).
 EXPORTED_SYMBOLS = (

@@ -49,6 +49,7 @@ struct gsr_context {
     // onesweep sort state: [0,1024) depth-sort digit counts, [1024,2048) tile-sort counts,
     // then the ticket word; look-back granules
     DevBuf sort_ctl, status;
+    DevBuf col_hist;  // column-first binning: per-(Gaussian block, column) pair counts
     uint32_t epoch = 0;  // tags the look-back granules of every onesweep pass
     // per-pair workspace
     DevBuf tile_keys, tile_vals, tile_keys_alt, tile_vals_alt;
@@ -82,6 +83,9 @@ struct gsr_context {
     // second tile-sort pass needs above the Gaussian id -- instead of a key and a value array
     // (needs the second-stream ranges; falls back when the bits do not fit)
     int packed_pairs = 1;
+    // GSR_OPT_COLUMN_PAIRS: the first tile-sort pass on (Gaussian, column) segments of the
+    // depth-sorted Gaussians instead of per pair (binning.hip k_col_count / k_col_scatter)
+    int column_pairs = 1;
     int color_blocks = 512;    // grid cap of the overlapped colour pass
     uint32_t blend_xcd_group = 16;  // tuning (env GSR_BLEND_XCD_GROUP)
     int blend_lean = 1;             // tuning (env GSR_BLEND_LEAN=0: record prefetch, 7 waves)
@@ -153,6 +157,9 @@ int reserve_P(gsr_context *ctx, int64_t P, hipStream_t s) {
     GSR_TRY(grow_zeroed(ctx, ctx->total, 16, s));  // [K (u64), look-back error flag (u32)]
     GSR_TRY(grow(ctx, ctx->pair_count, 8 * (size_t)((n + 255) / 256), s));  // per block
     GSR_TRY(grow(ctx, ctx->hist, (size_t)gsr_radix_hist_words(P) * 4, s));
+    // column-first binning's per-(block, column) counts: its own buffer, since reserve_K may
+    // regrow hist between the count and the scatter
+    GSR_TRY(grow(ctx, ctx->col_hist, (size_t)std::max<int64_t>(gsr_col_blocks(P), 1) * 256 * 4, s));
     GSR_TRY(grow(ctx, ctx->digit_total, 256 * 4 * GSR_RADIX_MAX_PASSES, s));  // a slice / pass
     GSR_TRY(grow(ctx, ctx->valid_count, 4, s));
     GSR_TRY(grow(ctx, ctx->bin, n * 16, s));
@@ -238,6 +245,8 @@ int gsr_create(gsr_context **out) {
     if (env_cb) ctx->color_blocks = std::atoi(env_cb);
     const char *env_ln = std::getenv("GSR_BLEND_LEAN");
     if (env_ln) ctx->blend_lean = std::atoi(env_ln);
+    const char *env_cp = std::getenv("GSR_COLUMN_PAIRS");
+    if (env_cp) ctx->column_pairs = std::atoi(env_cp);
     const char *env_pp = std::getenv("GSR_PACKED_PAIRS");
     if (env_pp) ctx->packed_pairs = std::atoi(env_pp);
     const char *env_ar = std::getenv("GSR_AUX_RANGES");
@@ -286,7 +295,7 @@ void gsr_destroy(gsr_context *ctx) {
                       &ctx->sort_ctl,      &ctx->status,
                       &ctx->tile_keys,     &ctx->tile_vals,
                       &ctx->tile_keys_alt, &ctx->tile_vals_alt, &ctx->ranges_local,
-                      &ctx->tile_diff};
+                      &ctx->tile_diff,     &ctx->col_hist};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &set : ctx->ev)
@@ -353,6 +362,10 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
     if (option == GSR_OPT_DEPTH_SORT_SHAPE) {
         if (value < 0 || value > 5) return fail(GSR_E_INVALID, "gsr_set_option: shape 0..5");
         ctx->depth_sort_shape = (int)value;
+        return GSR_OK;
+    }
+    if (option == GSR_OPT_COLUMN_PAIRS) {
+        ctx->column_pairs = value ? 1 : 0;
         return GSR_OK;
     }
     if (option == GSR_OPT_PACKED_PAIRS) {
@@ -616,10 +629,25 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     uint32_t *partials = static_cast<uint32_t *>(ctx->partials.p);
     uint64_t *d_total = static_cast<uint64_t *>(ctx->total.p);
     uint2 *rect_sorted = static_cast<uint2 *>(ctx->rect_sorted.p);
-    GSR_HIP(gsr_launch_scan_reduce(perm, pa.strip_rect, P, d_valid, partials, rect_sorted, s),
-            "scan launch");
-    GSR_HIP(gsr_launch_scan_partials(partials, gsr_scan_blocks(P), d_total, s), "scan launch");
-    const bool check_device_total = ctx->onesweep || dbg || ctx->late_K || !split_color;
+    // column-first pair generation: packed word = strip-local tile row << col_shift | id
+    const int ybits = rows_tiles > 1 ? bits_for(rows_tiles - 1) : 0;
+    const int col_shift = 32 - ybits;
+    const bool colpairs = ctx->column_pairs && !ctx->onesweep && ctx->fused_binning &&
+                          aux_ranges && gx <= 256 && rows_tiles <= 256 &&
+                          (col_shift == 32 || (uint64_t)P <= (1ull << col_shift));
+    if (colpairs) {  // per-column pair counts of the depth-sorted Gaussians + their scan
+        GSR_HIP(gsr_launch_col_pairs_count(perm, pa.strip_rect, P, d_valid, rect_sorted,
+                                           static_cast<uint32_t *>(ctx->col_hist.p), digit_total,
+                                           s),
+                "column count launch");
+    } else {
+        GSR_HIP(gsr_launch_scan_reduce(perm, pa.strip_rect, P, d_valid, partials, rect_sorted, s),
+                "scan launch");
+        GSR_HIP(gsr_launch_scan_partials(partials, gsr_scan_blocks(P), d_total, s),
+                "scan launch");
+    }
+    const bool check_device_total =
+        !colpairs && (ctx->onesweep || dbg || ctx->late_K || !split_color);
     if (check_device_total)  // onesweep's look-back flag (and, in debug mode, K) from the device
         GSR_HIP(hipMemcpyAsync(ctx->h_total, d_total, 16, hipMemcpyDeviceToHost, s),
                 "hipMemcpyAsync(num_rendered)");
@@ -658,10 +686,18 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     // pair keys are not stored (the ranges come from the second stream)
     const int high_bits = tplan.n == 2 ? tplan.nbits[1] : 0;
     const int pack_shift = 32 - high_bits;
-    const bool packed = ctx->packed_pairs && fused && aux_ranges && tplan.n <= 2 &&
+    const bool packed = !colpairs && ctx->packed_pairs && fused && aux_ranges && tplan.n <= 2 &&
                         (pack_shift == 32 || (uint64_t)P <= (1ull << pack_shift));
-    const uint32_t id_mask = (packed && pack_shift < 32) ? (1u << pack_shift) - 1u : 0xFFFFFFFFu;
-    if (K > 0) {
+    const int word_shift = colpairs ? col_shift : pack_shift;
+    const uint32_t id_mask = ((packed || colpairs) && word_shift < 32) ? (1u << word_shift) - 1u
+                                                                       : 0xFFFFFFFFu;
+    if (K > 0 && colpairs) {
+        GSR_HIP(gsr_launch_col_pairs_scatter(perm, rect_sorted, P, d_valid,
+                                             static_cast<const uint32_t *>(ctx->col_hist.p),
+                                             digit_total, col_shift, tv_alt, s),
+                "column scatter launch");
+        std::swap(tv, tv_alt);
+    } else if (K > 0) {
         GSR_HIP(gsr_launch_scan_down(perm, rect_sorted, partials, P, d_valid, d_total, bin,
                                      chunk_first, s),
                 "scan_down launch");
@@ -692,6 +728,13 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         GSR_HIP(gsr_onesweep_sort(&tk, &tv, &tk_alt, &tv_alt, (int64_t)K, 0, tbits,
                                   K > 0 ? GSR_HIST_READY : GSR_HIST_COUNT, onesweep_ws(ctx, 1), s),
                 "tile sort launch");
+    } else if (colpairs) {  // pass 2: the tile rows of the packed words, keys only
+        uint32_t *no_vals = nullptr, *no_vals_alt = nullptr;
+        if (ybits > 0)
+            GSR_HIP(gsr_radix_sort_pairs(&tv, &no_vals, &tv_alt, &no_vals_alt, (int64_t)K,
+                                         col_shift, 32, hist, digit_total, s,
+                                         ctx->tile_sort_shape, 0),
+                    "tile sort launch");
     } else if (packed) {  // the remaining tile bits of the packed words, keys only
         uint32_t *no_vals = nullptr, *no_vals_alt = nullptr;
         if (high_bits > 0)
@@ -752,7 +795,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     ctx->last_point_list = tv;
     ctx->last_tiles_local = tk;
     ctx->last_id_mask = id_mask;
-    ctx->last_packed = packed && K > 0;
+    ctx->last_packed = (packed || colpairs) && K > 0;
 
     ctx->have_forward = true;
     if (tmode) ++ctx->timed_frames;

@@ -376,6 +376,152 @@ __global__ __launch_bounds__(kFW * 64) void k_dup_scatter(
                                   sm, u.kv.keys, u.kv.vals);
 }
 
+// ---- column-first pair generation (GSR_OPT_COLUMN_PAIRS) ----------------------------------
+// The tile sort is LSD over (row, column): pass 1 by the column x, pass 2 by the row y.  Pass 1
+// needs no pair-level work: a Gaussian whose strip rect is [x0, x0+w) x [y0, y0+h) has h pairs
+// in each of its w columns, and in the stable column order those h pairs are contiguous (rows
+// ascending, as duplicateWithKeys emits them row-major).  So pass 1 runs on (Gaussian, column)
+// segments of h pairs:
+//   k_col_count   -- per block of kCG depth-sorted Gaussians, the pairs per column (a
+//                    difference array over the columns: two LDS atomics per Gaussian), and the
+//                    depth-ordered rect copy;
+//   k_rs_scan     -- per column, the exclusive scan across blocks (the radix sort's scan);
+//   k_col_scatter -- per block: rank its segments by column (stable, in LDS), turn segment
+//                    heights into pair offsets, and write every pair -- the packed word
+//                    (row << pack_shift) | Gaussian id that pass 2 sorts on -- at its column's
+//                    running position (consecutive lanes: consecutive pairs of a column).
+// It replaces the offsets scan, the per-chunk pair regeneration and the per-pair ranking of
+// the fused duplicate; the pair list is identical (each tile's pairs in depth order, then
+// Gaussian index; tiles row-major).
+constexpr int kCG = 256;                // depth-sorted Gaussians per block, one per thread
+constexpr int kCW = 4, kCIt = 8;        // segment ranking: 4 waves x 8 items
+constexpr int kCSeg = kCW * 64 * kCIt;  // 2048 segments ranked per round
+constexpr int kCQ = 8192;               // pairs mapped to their segment per window
+static_assert(kCG == kRadixBins, "one thread per column in the column scans");
+
+__global__ __launch_bounds__(kCG) void k_col_count(const uint32_t *__restrict__ perm,
+                                                   const uint2 *__restrict__ strip_rect,
+                                                   const uint32_t *__restrict__ d_n,
+                                                   uint2 *__restrict__ rect_sorted,
+                                                   uint32_t *__restrict__ hist, int64_t nb) {
+    __shared__ uint32_t s_diff[kRadixBins + 1];
+    __shared__ uint32_t s_tmp[4];
+    const int tid = threadIdx.x;
+    const int64_t n = *d_n;
+    const int64_t base = (int64_t)blockIdx.x * kCG;
+    if (base >= n) return;  // whole block (k_rs_scan reads blocks [0, ceil(n / kCG)) only)
+    for (int i = tid; i <= kRadixBins; i += kCG) s_diff[i] = 0u;
+    __syncthreads();
+    const int64_t e = base + tid;
+    if (e < n) {
+        const uint2 r = strip_rect[perm[e]];
+        rect_sorted[e] = r;
+        const uint32_t x0 = r.x & 0xFFFFu, w = r.x >> 16, h = r.y >> 16;
+        atomicAdd(&s_diff[x0], h);
+        atomicAdd(&s_diff[x0 + w], 0u - h);
+    }
+    __syncthreads();
+    uint32_t tot;
+    const uint32_t d = s_diff[tid];
+    hist[(int64_t)tid * nb + blockIdx.x] = block256_exclusive_scan(d, s_tmp, tot) + d;
+}
+
+__global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict__ perm,
+                                                     const uint2 *__restrict__ rect_sorted,
+                                                     const uint32_t *__restrict__ d_n,
+                                                     const uint32_t *__restrict__ hist, int64_t nb,
+                                                     const uint32_t *__restrict__ digit_total,
+                                                     int pack_shift, uint32_t *__restrict__ out) {
+    __shared__ uint32_t s_x0w[kCG], s_y0h[kCG], s_id[kCG], s_seg0[kCG + 1];
+    __shared__ uint32_t s_colbase[kRadixBins], s_colw0[kRadixBins];
+    __shared__ uint32_t s_keys[kCSeg], s_vals[kCSeg];  // the round's segments by column
+    __shared__ uint32_t s_wpre[kCSeg + 1];              // pair offset of each sorted segment
+    __shared__ uint16_t s_map[kCQ];                     // window pair -> sorted segment
+    __shared__ RadixTileSmem<kCW, kCIt> sm;
+    __shared__ uint32_t s_tmp[4];
+    const int tid = threadIdx.x;
+    const int64_t n = *d_n;
+    const int64_t base = (int64_t)blockIdx.x * kCG;
+    if (base >= n) return;
+    const int64_t e = base + tid;
+    const bool valid = e < n;
+    const uint2 r = valid ? rect_sorted[e] : make_uint2(0u, 0u);
+    s_x0w[tid] = r.x;
+    s_y0h[tid] = r.y;
+    s_id[tid] = valid ? perm[e] : 0u;
+    uint32_t tot;
+    // global start of column d for this block: all earlier columns, then earlier blocks
+    const uint32_t dstart = block256_exclusive_scan(digit_total[tid], s_tmp, tot);
+    s_colbase[tid] = dstart + hist[(int64_t)tid * nb + blockIdx.x];
+    // thread t owns segments [seg0, seg0 + w) (one per column of its rect)
+    uint32_t nseg;
+    const uint32_t seg0 = block256_exclusive_scan(r.x >> 16, s_tmp, nseg);
+    s_seg0[tid] = seg0;
+    if (tid == 0) s_seg0[kCG] = nseg;
+    __syncthreads();
+    for (uint32_t R = 0; R < nseg; R += kCSeg) {
+        const uint32_t rn = min((uint32_t)kCSeg, nseg - R);
+        uint32_t k[kCIt], v[kCIt];
+#pragma unroll
+        for (int j = 0; j < kCIt; ++j) {
+            const uint32_t slot = (uint32_t)((tid >> 6) * (kCSeg / kCW) + j * 64 + (tid & 63));
+            k[j] = 0xFFFFFFFFu;  // padding: largest column, after every real segment
+            v[j] = 0u;
+            if (slot < rn) {
+                const uint32_t sg = R + slot;
+                int lo = 0, hi = kCG - 1;  // last Gaussian whose first segment is <= sg
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (s_seg0[mid] <= sg) lo = mid;
+                    else hi = mid - 1;
+                }
+                k[j] = (s_x0w[lo] & 0xFFFFu) + (sg - s_seg0[lo]);
+                v[j] = (uint32_t)lo;
+            }
+        }
+        radix_tile_scatter<kCW, kCIt, false, false>(k, v, (int)rn, 0, 8, nullptr, 0, 0, nullptr,
+                                                    nullptr, nullptr, sm, s_keys, s_vals);
+        // pair offsets of the sorted segments (heights, exclusive prefix)
+        uint32_t hh[kCIt], hsum = 0;
+#pragma unroll
+        for (int j = 0; j < kCIt; ++j) {
+            const uint32_t p = (uint32_t)(tid * kCIt + j);
+            hh[j] = p < rn ? s_y0h[s_vals[p]] >> 16 : 0u;
+            hsum += hh[j];
+        }
+        uint32_t npairs;
+        uint32_t pre = block256_exclusive_scan(hsum, s_tmp, npairs);
+#pragma unroll
+        for (int j = 0; j < kCIt; ++j) {
+            s_wpre[tid * kCIt + j] = pre;
+            pre += hh[j];
+        }
+        if (tid == 0) s_wpre[kCSeg] = npairs;
+        __syncthreads();
+        s_colw0[tid] = sm.count[tid] ? s_wpre[sm.delta[tid]] : 0u;
+        __syncthreads();
+        for (uint32_t Q = 0; Q < npairs; Q += kCQ) {
+            const uint32_t qn = min((uint32_t)kCQ, npairs - Q);
+            for (uint32_t p = tid; p < rn; p += kCG) {
+                const uint32_t a0 = max(s_wpre[p], Q), a1 = min(s_wpre[p + 1], Q + qn);
+                for (uint32_t q = a0; q < a1; ++q) s_map[q - Q] = (uint16_t)p;
+            }
+            __syncthreads();
+            for (uint32_t i = tid; i < qn; i += kCG) {
+                const uint32_t q = Q + i, p = s_map[i];
+                const uint32_t c = s_keys[p], t = s_vals[p];
+                const uint32_t y = (s_y0h[t] & 0xFFFFu) + (q - s_wpre[p]);
+                out[s_colbase[c] + (q - s_colw0[c])] =
+                    (pack_shift < 32 ? y << pack_shift : 0u) | s_id[t];
+            }
+            __syncthreads();
+        }
+        // the next round continues every column where this one ended
+        if (sm.count[tid]) s_colbase[tid] += s_wpre[sm.delta[tid] + sm.count[tid]] - s_colw0[tid];
+        __syncthreads();
+    }
+}
+
 // upstream identifyTileRanges over the tile-sorted keys (ranges pre-zeroed).
 // 4 keys per thread (one 16-B load when aligned and complete).
 __global__ __launch_bounds__(kBlock) void k_ranges(const uint32_t *__restrict__ tile_keys,
@@ -643,5 +789,28 @@ hipError_t gsr_launch_fill_tiles(const uint2 *ranges, uint32_t n_tiles, uint32_t
                                  uint32_t *out, hipStream_t s) {
     if (n_tiles == 0) return hipSuccess;
     hipLaunchKernelGGL(k_fill_tiles, dim3(n_tiles), dim3(kBlock), 0, s, ranges, offset, out);
+    return hipGetLastError();
+}
+
+int64_t gsr_col_blocks(int64_t n) { return (n + kCG - 1) / kCG; }
+
+hipError_t gsr_launch_col_pairs_count(const uint32_t *perm, const uint2 *strip_rect, int64_t n_max,
+                                      const uint32_t *d_n, uint2 *rect_sorted, uint32_t *hist,
+                                      uint32_t *digit_total, hipStream_t s) {
+    const int64_t nb = gsr_col_blocks(n_max);
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_col_count, dim3((unsigned)nb), dim3(kCG), 0, s, perm, strip_rect, d_n,
+                       rect_sorted, hist, nb);
+    return gsr_launch_digit_scan_n(hist, nb, digit_total, d_n, kCG, s);
+}
+
+hipError_t gsr_launch_col_pairs_scatter(const uint32_t *perm, const uint2 *rect_sorted,
+                                        int64_t n_max, const uint32_t *d_n, const uint32_t *hist,
+                                        const uint32_t *digit_total, int pack_shift, uint32_t *out,
+                                        hipStream_t s) {
+    const int64_t nb = gsr_col_blocks(n_max);
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_col_scatter, dim3((unsigned)nb), dim3(kCG), 0, s, perm, rect_sorted, d_n,
+                       hist, nb, digit_total, pack_shift, out);
     return hipGetLastError();
 }

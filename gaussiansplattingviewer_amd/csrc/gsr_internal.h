@@ -305,6 +305,18 @@ hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_firs
                                     uint32_t *digit_total, uint32_t *keys_out, uint32_t *vals_out,
                                     uint2 *ranges_zero, uint32_t n_ranges, hipStream_t s,
                                     int pack_shift = -1);
+// Column-first pair generation (binning.hip): pass 1 of the tile sort on (Gaussian, column)
+// segments of the depth-sorted Gaussians.  hist: gsr_col_blocks(n_max) * 256 words.
+int64_t gsr_col_blocks(int64_t n);
+hipError_t gsr_launch_col_pairs_count(const uint32_t *perm, const uint2 *strip_rect, int64_t n_max,
+                                      const uint32_t *d_n, uint2 *rect_sorted, uint32_t *hist,
+                                      uint32_t *digit_total, hipStream_t s);
+hipError_t gsr_launch_col_pairs_scatter(const uint32_t *perm, const uint2 *rect_sorted,
+                                        int64_t n_max, const uint32_t *d_n, const uint32_t *hist,
+                                        const uint32_t *digit_total, int pack_shift, uint32_t *out,
+                                        hipStream_t s);
+hipError_t gsr_launch_digit_scan_n(uint32_t *hist, int64_t nb, uint32_t *digit_total,
+                                   const uint32_t *d_n, int64_t tile, hipStream_t s);
 // Packed pair lists (gsr_launch_dup_sort_pass with pack_shift >= 0): ids = packed & mask;
 // tile ids (offset + strip-local tile) from the tile ranges.
 hipError_t gsr_launch_unpack_ids(const uint32_t *packed, int64_t K, uint32_t mask, uint32_t *out,

@@ -385,6 +385,14 @@ hipError_t gsr_launch_digit_scan(uint32_t *hist, int64_t nb, uint32_t *digit_tot
     return hipGetLastError();
 }
 
+// k_rs_scan over nb columns whose live length is ceil(*d_n / tile) (column-first binning).
+hipError_t gsr_launch_digit_scan_n(uint32_t *hist, int64_t nb, uint32_t *digit_total,
+                                   const uint32_t *d_n, int64_t tile, hipStream_t s) {
+    hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, nb, digit_total,
+                       RsCount{nb, nullptr, nullptr, d_n}, tile);
+    return hipGetLastError();
+}
+
 int64_t gsr_radix_hist_words(int64_t n) {
     const int64_t nb = (n + 1023) / 1024;  // smallest tile shape (4 waves x 4 items)
     return (nb < 1 ? 1 : nb) * kRadix;

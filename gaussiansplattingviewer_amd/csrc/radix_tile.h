@@ -36,6 +36,7 @@ struct RadixTileSmem {
     static constexpr int kT = kW * 64 * kIt;
     uint32_t wcnt[kW][kRadixBins];
     uint32_t delta[kRadixBins];
+    uint32_t count[kRadixBins];  // kToGlobal = false: digit counts of the tile
     uint32_t tmp[2 * kW + 1];
 };
 
@@ -52,7 +53,10 @@ struct RadixTileSmem {
 // vals_out == nullptr: keys only (v is ignored).
 constexpr uint32_t kDropKey = 0xFFFFFFFFu;
 
-template <int kW, int kIt, bool kDrop = false>
+// kToGlobal = false (in-LDS ranking, binning.hip k_col_scatter): stop once the tile sits in
+// s_keys / s_vals in digit order; hist, digit_total, keys_out and vals_out are not used,
+// sm.delta[d] is then the tile-local start of digit d and sm.count[d] its count.
+template <int kW, int kIt, bool kDrop = false, bool kToGlobal = true>
 __device__ __forceinline__ void radix_tile_scatter(
     const uint32_t (&k)[kIt], const uint32_t (&v)[kIt], int valid, int shift, int nbits,
     const uint32_t *__restrict__ hist, int64_t nb, uint32_t tile,
@@ -99,10 +103,17 @@ __device__ __forceinline__ void radix_tile_scatter(
         const uint32_t local_start =
             blockw_exclusive_scan<kW>(d < kRadixBins ? sum : 0u, sm.tmp, tile_total);
         if (kDrop && tid == 0) sm.tmp[2 * kW] = tile_total;
-        const uint32_t digit_start = blockw_exclusive_scan<kW>(
-            d < kRadixBins ? digit_total[d] : 0u, sm.tmp + kW, all_total);
+        uint32_t digit_start = 0;
+        if (kToGlobal)
+            digit_start = blockw_exclusive_scan<kW>(d < kRadixBins ? digit_total[d] : 0u,
+                                                    sm.tmp + kW, all_total);
         if (d < kRadixBins) {
-            sm.delta[d] = digit_start + hist[(int64_t)d * nb + tile] - local_start;
+            if (kToGlobal) {
+                sm.delta[d] = digit_start + hist[(int64_t)d * nb + tile] - local_start;
+            } else {
+                sm.delta[d] = local_start;
+                sm.count[d] = sum;
+            }
             uint32_t run = local_start;
 #pragma unroll
             for (int i = 0; i < kW; ++i) {
@@ -118,9 +129,10 @@ __device__ __forceinline__ void radix_tile_scatter(
         const uint32_t d = (k[j] >> shift) & mask;
         const uint32_t pos = sm.wcnt[w][d] + rank[j];
         s_keys[pos] = k[j];
-        if (vals_out) s_vals[pos] = v[j];
+        if (vals_out || !kToGlobal) s_vals[pos] = v[j];
     }
     __syncthreads();
+    if (!kToGlobal) return;
     const int n_out = kDrop ? (int)sm.tmp[2 * kW] : valid;  // kept elements of the tile
     for (int i = tid; i < n_out; i += kThreads) {
         const uint32_t kk = s_keys[i];

@@ -215,9 +215,15 @@ const char *gsr_stage_name(int i);
  *     written once by the fused duplicate and sorted keys-only; used when the tile ranges come
  *     from the second stream and the bits fit (P <= 2^(32 - second-pass bits)), else key and
  *     value arrays.  Identical results. */
+/*   GSR_OPT_COLUMN_PAIRS (default 1): the first tile-sort pass (by tile column) runs on
+ *     (Gaussian, column) segments of the depth-sorted Gaussians -- a per-column difference-
+ *     array count and a segment scatter -- instead of regenerating and ranking every pair; the
+ *     second pass sorts packed (tile row, Gaussian id) words.  Needs the second-stream ranges,
+ *     <= 256 tile columns and rows per strip, P <= 2^(32 - row bits).  Identical results. */
 enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_SORT_ONESWEEP = 3,
        GSR_OPT_TILE_SORT_SHAPE = 4, GSR_OPT_FUSED_BINNING = 5, GSR_OPT_BLEND_WAVE_QUADRANTS = 6,
-       GSR_OPT_DEPTH_SORT_SHAPE = 7, GSR_OPT_SPLIT_COLOR = 8, GSR_OPT_PACKED_PAIRS = 9 };
+       GSR_OPT_DEPTH_SORT_SHAPE = 7, GSR_OPT_SPLIT_COLOR = 8, GSR_OPT_PACKED_PAIRS = 9,
+       GSR_OPT_COLUMN_PAIRS = 10 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
 
 #ifdef __cplusplus

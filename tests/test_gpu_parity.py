@@ -227,7 +227,8 @@ def test_headline_config_c3(gpu, c3_oracle, fast):
 
 VARIANTS = {  # [(option, alternative value, default), ...]
     "onesweep": [(_lib.GSR_OPT_SORT_ONESWEEP, 1, 0)],
-    "unpacked": [(_lib.GSR_OPT_PACKED_PAIRS, 0, 1)],
+    "per_pair": [(_lib.GSR_OPT_COLUMN_PAIRS, 0, 1)],
+    "unpacked": [(_lib.GSR_OPT_COLUMN_PAIRS, 0, 1), (_lib.GSR_OPT_PACKED_PAIRS, 0, 1)],
     "unfused": [(_lib.GSR_OPT_FUSED_BINNING, 0, 1)],
     "tile_shape0": [(_lib.GSR_OPT_TILE_SORT_SHAPE, 0, 3)],
     "tile_shape5": [(_lib.GSR_OPT_TILE_SORT_SHAPE, 5, 3)],
@@ -273,7 +274,7 @@ def test_sort_implementations_agree(gpu, variant, size):
         np.testing.assert_array_equal(alt[k], ref[k], err_msg=k)
 
 
-@pytest.mark.parametrize("variant", ["default", "unpacked", "onesweep", "unfused"])
+@pytest.mark.parametrize("variant", ["default", "per_pair", "unpacked", "onesweep", "unfused"])
 def test_long_tile_lists_and_depth_ties(gpu, oracle_mod, variant):
     """Tiles covered by more than 2048 splats (multi-chunk digit runs in the tile sort, long
     blend lists) and half of the Gaussians at one depth (ties: upstream orders them by
