@@ -389,14 +389,13 @@ __global__ __launch_bounds__(kFW * 64) void k_dup_scatter(
 //   k_col_scatter -- per block: rank its segments by column (stable, in LDS), turn segment
 //                    heights into pair offsets, and write every pair -- the packed word
 //                    (row << pack_shift) | Gaussian id that pass 2 sorts on -- at its column's
-//                    running position (consecutive lanes: consecutive pairs of a column).
+//                    running position (one thread per segment, its h pairs contiguous).
 // It replaces the offsets scan, the per-chunk pair regeneration and the per-pair ranking of
 // the fused duplicate; the pair list is identical (each tile's pairs in depth order, then
 // Gaussian index; tiles row-major).
 constexpr int kCG = 256;                // depth-sorted Gaussians per block, one per thread
 constexpr int kCW = 4, kCIt = 8;        // segment ranking: 4 waves x 8 items
 constexpr int kCSeg = kCW * 64 * kCIt;  // 2048 segments ranked per round
-constexpr int kCQ = 8192;               // pairs mapped to their segment per window
 static_assert(kCG == kRadixBins, "one thread per column in the column scans");
 
 __global__ __launch_bounds__(kCG) void k_col_count(const uint32_t *__restrict__ perm,
@@ -436,7 +435,6 @@ __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict_
     __shared__ uint32_t s_colbase[kRadixBins], s_colw0[kRadixBins];
     __shared__ uint32_t s_keys[kCSeg], s_vals[kCSeg];  // the round's segments by column
     __shared__ uint32_t s_wpre[kCSeg + 1];              // pair offset of each sorted segment
-    __shared__ uint16_t s_map[kCQ];                     // window pair -> sorted segment
     __shared__ RadixTileSmem<kCW, kCIt> sm;
     __shared__ uint32_t s_tmp[4];
     const int tid = threadIdx.x;
@@ -500,22 +498,17 @@ __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict_
         __syncthreads();
         s_colw0[tid] = sm.count[tid] ? s_wpre[sm.delta[tid]] : 0u;
         __syncthreads();
-        for (uint32_t Q = 0; Q < npairs; Q += kCQ) {
-            const uint32_t qn = min((uint32_t)kCQ, npairs - Q);
-            for (uint32_t p = tid; p < rn; p += kCG) {
-                const uint32_t a0 = max(s_wpre[p], Q), a1 = min(s_wpre[p + 1], Q + qn);
-                for (uint32_t q = a0; q < a1; ++q) s_map[q - Q] = (uint16_t)p;
-            }
-            __syncthreads();
-            for (uint32_t i = tid; i < qn; i += kCG) {
-                const uint32_t q = Q + i, p = s_map[i];
-                const uint32_t c = s_keys[p], t = s_vals[p];
-                const uint32_t y = (s_y0h[t] & 0xFFFFu) + (q - s_wpre[p]);
-                out[s_colbase[c] + (q - s_colw0[c])] =
-                    (pack_shift < 32 ? y << pack_shift : 0u) | s_id[t];
-            }
-            __syncthreads();
+        // one thread per sorted segment (consecutive lanes: consecutive segments, so within a
+        // column consecutive destination runs); each writes its h pairs
+        for (uint32_t p = tid; p < rn; p += kCG) {
+            const uint32_t c = s_keys[p], t = s_vals[p];
+            const uint32_t y0h = s_y0h[t], id = s_id[t];
+            const uint32_t dst = s_colbase[c] + (s_wpre[p] - s_colw0[c]);
+            const uint32_t y0 = y0h & 0xFFFFu, h = y0h >> 16;
+            for (uint32_t r = 0; r < h; ++r)
+                out[dst + r] = (pack_shift < 32 ? (y0 + r) << pack_shift : 0u) | id;
         }
+        __syncthreads();  // every thread has read this round's column bases
         // the next round continues every column where this one ended
         if (sm.count[tid]) s_colbase[tid] += s_wpre[sm.delta[tid] + sm.count[tid]] - s_colw0[tid];
         __syncthreads();
