@@ -657,15 +657,25 @@ __global__ __launch_bounds__(kDiffThreads) void k_tile_diff(const uint2 *__restr
     for (uint32_t c = threadIdx.x; c < cells; c += kDiffThreads) s_diff[c] = 0u;
     __syncthreads();
     const int64_t b0 = P * blockIdx.x / gridDim.x, b1 = P * (blockIdx.x + 1) / gridDim.x;
-    for (int64_t i = b0 + threadIdx.x; i < b1; i += kDiffThreads) {
-        const uint2 r = strip_rect[i];
-        if (r.x == 0u) continue;  // no pairs in the strip (a rect with pairs has width > 0)
-        const uint32_t x0 = r.x & 0xFFFFu, x1 = x0 + (r.x >> 16);
-        const uint32_t y0 = r.y & 0xFFFFu, y1 = y0 + (r.y >> 16);
-        atomicAdd(&s_diff[y0 * w1 + x0], 1u);
-        atomicAdd(&s_diff[y0 * w1 + x1], 0xFFFFFFFFu);  // -1 (mod 2^32)
-        atomicAdd(&s_diff[y1 * w1 + x0], 0xFFFFFFFFu);
-        atomicAdd(&s_diff[y1 * w1 + x1], 1u);
+    // 4 rects per thread and step, their loads issued together (a block covers P / 64)
+    constexpr int kU = 4;
+    for (int64_t i = b0 + threadIdx.x; i < b1; i += kU * kDiffThreads) {
+        uint2 r[kU];
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+            const int64_t j = i + (int64_t)k * kDiffThreads;
+            r[k] = j < b1 ? strip_rect[j] : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+            if (r[k].x == 0u) continue;  // no pairs in the strip (a rect with pairs has width > 0)
+            const uint32_t x0 = r[k].x & 0xFFFFu, x1 = x0 + (r[k].x >> 16);
+            const uint32_t y0 = r[k].y & 0xFFFFu, y1 = y0 + (r[k].y >> 16);
+            atomicAdd(&s_diff[y0 * w1 + x0], 1u);
+            atomicAdd(&s_diff[y0 * w1 + x1], 0xFFFFFFFFu);  // -1 (mod 2^32)
+            atomicAdd(&s_diff[y1 * w1 + x0], 0xFFFFFFFFu);
+            atomicAdd(&s_diff[y1 * w1 + x1], 1u);
+        }
     }
     __syncthreads();
     uint32_t *dst = partial + (int64_t)blockIdx.x * cells;

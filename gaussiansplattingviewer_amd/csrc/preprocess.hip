@@ -42,10 +42,15 @@ __device__ __forceinline__ float3 color_from_sh(float3 pos, const float *campos,
     if (vec_ok) {  // M == 16 and 16-B aligned rows
         const float4 *v = reinterpret_cast<const float4 *>(sh);
         const int nvec = (ncoef * 3 + 3) >> 2;
+        // all 12 loads unconditionally (the row always holds 16 coefficients), so they issue
+        // together instead of one predicated round trip each; unused ones are zeroed after
+        float4 rowv[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) rowv[i] = v[i];
 #pragma unroll
         for (int i = 0; i < 12; ++i) {
             float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (i < nvec) q = v[i];
+            if (i < nvec) q = rowv[i];
             c[4 * i + 0] = q.x;
             c[4 * i + 1] = q.y;
             c[4 * i + 2] = q.z;
