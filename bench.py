@@ -12,9 +12,11 @@ launched by torch.distributed.run) the frame's 16-px tile rows are split into N 
 rank renders its strip and rank 0 gathers the frame over RCCL (strong scaling: the frame is
 fixed, N grows).
 
-Prints ONE JSON line on rank 0.  `roofline` is for the dominant kernel stage, from HIP events
-recorded on the forward's stream over the timed region; `cpu_baseline` times the CPU oracle
-(oracle/, a C port of the same forward, 1 thread) on rank 0 at N = 1.
+Prints ONE JSON line on rank 0.  `roofline` is for the dominant kernel (the blend): its
+algorithmic bytes over its launch duration from HIP events of a serial pass, with measured HBM
+traffic and a VALU roof from committed rocprofv3 PMC profiles; `cpu_baseline` times, on rank 0
+at N = 1, the reference's own CPU sort path (renderer_ogl.py:10-19, restated and pinned in
+oracle/) and the CPU oracle of the whole forward (oracle/, a C port, 1 thread).
 """
 from __future__ import annotations
 
@@ -97,8 +99,11 @@ class Scene:
         n_cams = 1000 if cam_kind == "orbit" else 1
         for i in range(n_cams):
             eye = orbit_eye(i, 1000) if cam_kind == "orbit" else (0.0, 0.0, 4.0)
-            view, proj, campos, tx, ty = cuda_camera_inputs(static_camera(W, H, eye))
+            cam = static_camera(W, H, eye)
+            view, proj, campos, tx, ty = cuda_camera_inputs(cam)
             self.cams.append((up(view), up(proj), up(campos), tx, ty, (view, proj, campos)))
+            if i == 0:  # the GL view (math layout) the OpenGL backend's sort receives
+                self.gl_view0 = np.asarray(cam.get_view_matrix(), dtype=np.float32)
 
     def render(self, step, tile_rows=None, slot=0, out_color=None):
         view, proj, campos, tx, ty, _ = self.cams[step % len(self.cams)]
@@ -130,6 +135,34 @@ def measured_traffic(stage, config, default_opts):
     return int(rec["read_bytes_x2"] + rec["write_bytes"]), os.path.relpath(TRAFFIC_PROFILE, REPO)
 
 
+# VALU roofline of the blend ("additionally reported against FP32 VALU
+# peak"): per-launch SQ counters of the blend kernel from a committed PMC profile of this
+# command (tools/pmc_sq.sh + tools/sq_summary.py --json).  achieved = SQ_INSTS_VALU (wave64
+# instructions) x 64 lanes / launch time; peak = 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz =
+# 78.6 T lane-instructions/s (the 157.3 TFLOP/s FP32 vector peak counts an FMA as 2 flops).
+# busy = SQ_ACTIVE_INST_VALU (quad-cycles) x 4 / (1024 SIMDs x kernel cycles).
+VALU_PROFILE = os.path.join(REPO, "profiles", "r02_c3_blend_sq.json")
+VALU_PEAK_T = 256 * 4 * 32 * 2.4e9 / 1e12
+
+
+def valu_roofline(stage, launch_ms, config, default_opts):
+    if stage != "blend" or config != "c3" or not default_opts or not os.path.exists(VALU_PROFILE):
+        return None
+    prof = json.load(open(VALU_PROFILE))
+    c = prof["per_launch"]
+    lane_instr = c["SQ_INSTS_VALU"] * 64
+    ach = lane_instr / (launch_ms * 1e-3) / 1e12
+    cyc = c["GRBM_GUI_ACTIVE"] / 8  # summed over the 8 XCDs
+    out = {"bound": "valu", "achieved": round(ach, 3), "peak": round(VALU_PEAK_T, 3),
+           "unit": "T lane-instr/s", "frac": round(ach / VALU_PEAK_T, 4),
+           "valu_wave_instr_per_launch": int(c["SQ_INSTS_VALU"]),
+           "waves_per_launch": int(c["SQ_WAVES"]),
+           "source": os.path.relpath(VALU_PROFILE, REPO)}
+    if "SQ_ACTIVE_INST_VALU" in c:
+        out["valu_busy"] = round(c["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / cyc, 4)
+    return out
+
+
 def algorithmic_bytes(P, P_f, P_v, K, T, W, H, sh_bytes):
     """algorithmic HBM bytes per stage of one frame (the SH read of the
     preprocess is the "color" stage, which runs on the second stream)."""
@@ -145,12 +178,43 @@ def algorithmic_bytes(P, P_f, P_v, K, T, W, H, sh_bytes):
     }
 
 
+def host_cpu():
+    """CPU model (lscpu "Model name", else /proc/cpuinfo) and the BLAS / OpenMP thread env."""
+    model = None
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        model = next((l.split(":", 1)[1].strip() for l in out.splitlines()
+                      if l.startswith("Model name")), None)
+    except Exception:
+        pass
+    if model is None and os.path.exists("/proc/cpuinfo"):
+        model = next((l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
+                      if l.startswith("model name")), None)
+    env = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS",
+                                          "MKL_NUM_THREADS")}
+    return model or platform.processor() or platform.machine(), env
+
+
 def cpu_baseline(scene, min_seconds):
-    """The oracle (C port of the forward, single thread) on a bounded sample of the same
-    workload: whole frames of the same scene and camera until min_seconds have elapsed."""
+    """Two CPU legs on rank 0's host cores (the checker's code, timed here only as baselines):
+
+    1. the reference's own CPU path -- the OpenGL backend's per-frame depth sort
+       `_sort_gaussian_cpu` (renderer_ogl.py:10-19), as restated in `oracle.sort_gaussian_cpu`
+       (bit-exact to outputs captured from the reference, tests/golden/sort_backend.npz), on the
+       scene's P Gaussians and GL view: one warm-up, then the median of 5 calls;
+    2. the full forward on the CPU -- oracle/gsr_oracle.c, the C restatement of the upstream
+       rasterizer the viewer's CUDA backend calls (1 thread): whole frames of the same scene and
+       camera, at least 3 frames and at least min_seconds.  `value` is this leg's frame rate."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle  # the checker's C restatement; timed here only as the CPU baseline
+    import oracle
     g = scene.host
+    ts = []
+    for _ in range(6):
+        t0 = time.perf_counter()
+        oracle.sort_gaussian_cpu(g.xyz, scene.gl_view0)
+        ts.append(time.perf_counter() - t0)
+    sort_ms = 1e3 * float(np.median(ts[1:]))
     view, proj, campos = scene.cams[0][5]
     tx, ty = scene.cams[0][3], scene.cams[0][4]
     frames, t0 = 0, time.perf_counter()
@@ -159,13 +223,19 @@ def cpu_baseline(scene, min_seconds):
                        sh_degree=scene.deg, scales=g.scale, rotations=g.rot)
         frames += 1
         el = time.perf_counter() - t0
-        if el >= min_seconds or frames >= 3:
+        if el >= min_seconds and frames >= 3:
             break
+    model, env = host_cpu()
     return {"value": round(frames / el, 5), "unit": "frames/sec", "cores": 1, "kind": "port",
             "sample": f"{frames} full frame(s) of the {scene.P}-Gaussian {scene.W}x{scene.H} "
-                      f"SH{scene.deg} scene through oracle/gsr_oracle.c (1 thread, {el:.1f} s); "
-                      f"host {platform.processor() or platform.machine()}, "
-                      f"os.cpu_count()={os.cpu_count()}"}
+                      f"SH{scene.deg} scene through oracle/gsr_oracle.c (1 thread, {el:.1f} s)",
+            "reference_sort": {
+                "fn": "renderer_ogl._sort_gaussian_cpu (renderer_ogl.py:10-19) via "
+                      "oracle.sort_gaussian_cpu, pinned to reference-captured outputs",
+                "ms_median_of_5": round(sort_ms, 3), "calls_per_sec": round(1e3 / sort_ms, 3),
+                "P": scene.P, "threads": "numpy argsort is single-threaded; the stacked matmul "
+                                         "follows the BLAS / OpenMP env below"},
+            "host": {"cpu_model": model, "os_cpu_count": os.cpu_count(), "thread_env": env}}
 
 
 def main():
@@ -307,9 +377,12 @@ def main():
     # second-stream interval -- pair count, SH colour and tile ranges, overlapped with the depth
     # sort -- so its event time is not one kernel's launch duration.)
     dominant = "blend" if stage_ms.get("blend", 0.0) > 0.0 else max(stage_ms, key=stage_ms.get)
-    dom_ms = blend_ms_timed if dominant == "blend" else stage_ms[dominant]
+    # Launch duration for the roofline: the serial stage pass (one frame at a time, events on
+    # the forward's stream bracket the kernel alone), which is what a rocprofv3 kernel trace of
+    # a serial run reports for it (profiles/).  The timed region's blend events (two frames in
+    # flight) also count the other frame's kernels sharing the CUs; reported beside it.
+    dom_ms = stage_ms[dominant]
     ach = alg[dominant] / (dom_ms * 1e-3) / 1e9
-
     default_opts = not (args.sort_shape is not None or args.depth_sort_shape is not None or
                         args.onesweep or args.unfused or args.blend_blocks or args.inline_color or
                         args.blend != "fast")
@@ -351,7 +424,11 @@ def main():
                      "traffic_source": traffic_src,
                      "bytes_per_launch": int(alg[dominant]),
                      "launch_ms": round(dom_ms, 5),
-                     "frame_achieved_gbs": round(sum(alg.values()) / (t_max / args.steps) / 1e9, 2)},
+                     "launch_ms_source": "serial stage pass: HIP events around the kernel on "
+                                         "the forward's stream, one frame at a time; frac uses it",
+                     "launch_ms_inflight": round(blend_ms_timed, 5),
+                     "frame_achieved_gbs": round(sum(alg.values()) / (t_max / args.steps) / 1e9, 2),
+                     "valu": valu_roofline(dominant, dom_ms, args.config, default_opts)},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

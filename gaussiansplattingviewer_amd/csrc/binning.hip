@@ -9,6 +9,8 @@
 // by Gaussian index, exactly as upstream's stable 64-bit sort orders it, so point lists and
 // ranges are bit-identical while the K-sized sort moves 8-B pairs over 2 passes instead of
 // 12-B pairs over 6.
+#include <atomic>
+
 #include "radix_tile.h"
 
 using namespace gsr;
@@ -743,17 +745,22 @@ hipError_t gsr_launch_tile_ranges_aux(const uint2 *strip_rect, int64_t P, uint32
     const uint32_t cells = gsr_tile_diff_cells(gx, rows);
     const size_t lds = (size_t)cells * 4;
     if (cells > kTileDiffMaxCells) return hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_tile_diff),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           kTileDiffMaxCells * 4);
+    // the > 64 KiB dynamic-LDS attribute is per (function, device): one bit per device, set
+    // atomically (setting it twice from racing threads is harmless)
+    static std::atomic<uint64_t> attr_done{0};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const uint64_t bit = dev < 64 ? (1ull << dev) : 0ull;
+    if (!bit || !(attr_done.load(std::memory_order_acquire) & bit)) {
+        e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_tile_diff),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kTileDiffMaxCells * 4);
         if (e == hipSuccess)
             e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_tile_ranges_from_diff),
                                     hipFuncAttributeMaxDynamicSharedMemorySize,
                                     kTileDiffMaxCells * 4);
         if (e != hipSuccess) return e;
-        attr_set = true;
+        attr_done.fetch_or(bit, std::memory_order_release);
     }
     hipLaunchKernelGGL(k_tile_diff, dim3(kTileDiffBlocks), dim3(kDiffThreads), lds, s, strip_rect,
                        P, gx, rows, partial);

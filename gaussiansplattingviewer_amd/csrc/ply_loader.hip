@@ -167,11 +167,16 @@ int parse_header(const Mapped &m, Header &h) {
     bool in_vertex = false, seen_vertex = false, have_format = false;
     int64_t skip_bytes_before = 0;  // fixed-size elements before the vertex element
     int64_t cur_count = 0;
-    int cur_stride = 0;
+    int64_t cur_stride = 0;
     bool cur_has_list = false;
+    // Counts and strides come from an untrusted header: every product and sum is bounded by
+    // the file size before it is formed (no wrap in the size_t / int64 arithmetic below).
     auto close_element = [&]() -> int {
         if (!in_vertex && cur_count > 0 && !seen_vertex) {
             if (cur_has_list) return ply_fail(GSR_E_INVALID, "list property before the vertex element");
+            const int64_t room = (int64_t)n - skip_bytes_before;  // skip_bytes_before <= n
+            if (cur_stride > 0 && cur_count > room / cur_stride)
+                return ply_fail(GSR_E_INVALID, "PLY file shorter than its elements");
             skip_bytes_before += cur_count * cur_stride;
         }
         return GSR_OK;
@@ -220,9 +225,10 @@ int parse_header(const Mapped &m, Header &h) {
             PType pt;
             int sz;
             if (!ptype_of(t, pt, sz)) return ply_fail(GSR_E_INVALID, std::string("unknown type ") + t);
-            if (in_vertex) h.props.push_back({name, pt, sz, cur_stride});
+            if (cur_stride > (int64_t)n) return ply_fail(GSR_E_INVALID, "PLY element wider than the file");
+            if (in_vertex) h.props.push_back({name, pt, sz, (int)cur_stride});
             cur_stride += sz;
-            if (in_vertex) h.stride = cur_stride;
+            if (in_vertex) h.stride = (int)cur_stride;
         } else if (w == "end_header") {
             break;
         } else {
@@ -234,8 +240,13 @@ int parse_header(const Mapped &m, Header &h) {
     h.data_offset = pos + (h.format == Header::ASCII ? 0 : (size_t)skip_bytes_before);
     if (h.format == Header::ASCII && skip_bytes_before > 0)
         return ply_fail(GSR_E_INVALID, "ascii PLY with elements before the vertex element");
+    // ascii: every value takes at least two bytes ("0 "; the file's last one may end at EOF)
+    if (h.format == Header::ASCII && !h.props.empty() &&
+        (uint64_t)h.count > (m.size - std::min(m.size, h.data_offset) + 1) / (2 * h.props.size()))
+        return ply_fail(GSR_E_INVALID, "ascii PLY shorter than its vertex data");
     if (h.format != Header::ASCII &&
-        h.data_offset + (size_t)h.count * (size_t)h.stride > m.size)
+        (h.data_offset > m.size ||
+         (h.stride > 0 && (uint64_t)h.count > (m.size - h.data_offset) / (size_t)h.stride)))
         return ply_fail(GSR_E_INVALID, "PLY file shorter than its vertex data");
     return GSR_OK;
 }
@@ -451,11 +462,19 @@ int convert_ascii(const Mapped &m, const Header &h, const Layout &L, float *xyz,
         for (size_t k = 0; k < h.props.size(); ++k) {
             while (s < end && (*s == ' ' || *s == '\n' || *s == '\r' || *s == '\t')) ++s;
             if (s >= end) return ply_fail(GSR_E_INVALID, "ascii PLY shorter than its vertex data");
+            // the token, copied out NUL-terminated: strtod must not run past the mapping
+            const char *t = s;
+            while (t < end && !(*t == ' ' || *t == '\n' || *t == '\r' || *t == '\t')) ++t;
+            char tok[64];
+            const size_t len = (size_t)(t - s);
+            if (len >= sizeof(tok)) return ply_fail(GSR_E_INVALID, "bad number in ascii PLY");
+            std::memcpy(tok, s, len);
+            tok[len] = '\0';
             char *stop = nullptr;
             // like plyfile (numpy text parsing): as float64, then the property's type
-            const double d = std::strtod(s, &stop);
-            if (stop == s) return ply_fail(GSR_E_INVALID, "bad number in ascii PLY");
-            s = stop;
+            const double d = std::strtod(tok, &stop);
+            if (stop != tok + len || len == 0) return ply_fail(GSR_E_INVALID, "bad number in ascii PLY");
+            s = t;
             double val = d;
             switch (h.props[k].type) {
                 case PType::F32: val = (double)(float)d; break;

@@ -167,15 +167,35 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
                         cov3Ds_precomp, raster_settings: GaussianRasterizationSettings):
-    """upstream rasterize_gaussians(...) -> (color, radii)."""
-    del means2D  # only carries screen-space gradients upstream
-    res = rasterize_gaussians_native(
-        raster_settings.bg, means3D, colors_precomp, opacities, scales, rotations,
-        raster_settings.scale_modifier, cov3Ds_precomp, raster_settings.viewmatrix,
-        raster_settings.projmatrix, raster_settings.tanfovx, raster_settings.tanfovy,
-        raster_settings.image_height, raster_settings.image_width, sh, raster_settings.sh_degree,
-        raster_settings.campos, raster_settings.prefiltered, raster_settings.debug)
-    return res.color, res.radii
+    """upstream rasterize_gaussians(...) -> (color, radii), through _RasterizeGaussians."""
+    return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales,
+                                     rotations, cov3Ds_precomp, raster_settings)
+
+
+class _RasterizeGaussians(torch.autograd.Function):
+    """upstream `_RasterizeGaussians`: packs the settings into `_C.rasterize_gaussians`'s
+    argument tuple and keeps (color, radii) of its 6-tuple.  Forward only (the viewer renders
+    under `torch.no_grad()`, renderer_cuda.py:214)."""
+
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
+                cov3Ds_precomp, raster_settings):
+        from . import _C
+        del means2D  # only carries screen-space gradients upstream
+        rs = raster_settings
+        args = (rs.bg, means3D, colors_precomp, opacities, scales, rotations, rs.scale_modifier,
+                cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy,
+                rs.image_height, rs.image_width, sh, rs.sh_degree, rs.campos, rs.prefiltered,
+                rs.debug)
+        num_rendered, color, radii, geom, binning, img = _C.rasterize_gaussians(*args)
+        ctx.num_rendered = num_rendered
+        ctx.mark_non_differentiable(radii)
+        return color, radii
+
+    @staticmethod
+    def backward(ctx, grad_color, grad_radii):
+        raise RuntimeError("gaussiansplattingviewer_amd renders forward only (the viewer never "
+                           "differentiates, renderer_cuda.py:214)")
 
 
 class GaussianRasterizer(torch.nn.Module):
@@ -218,11 +238,11 @@ class GaussianRasterizer(torch.nn.Module):
                                    rotations, cov3D_precomp, rs)
 
 
-def binning_state(device_index: int = 0):
-    """(point_list, point_tiles, ranges [T,2]) of the last forward on a device, as device
-    int32 tensors holding the uint32 values (test / debug helper)."""
+def binning_state(device_index: int = 0, slot: int = 0):
+    """(point_list, point_tiles, ranges [T,2]) of the last forward on a device's context slot,
+    as device int32 tensors holding the uint32 values (test / debug helper)."""
     lib = _lib.load_library()
-    ctx = _lib.context(device_index)
+    ctx = _lib.context(device_index, slot)
     K = ctypes.c_int64()
     T = ctypes.c_int32()
     stream = ctypes.c_void_p(torch.cuda.current_stream(device_index).cuda_stream)

@@ -14,10 +14,17 @@ Captured:
   camera.npz        -- util.Camera.get_project_matrix / get_htanfovxy_focal (util.py:82-113)
                        at the four benchmark resolutions.
   naive_gaussian.npz-- util_gau.naive_gaussian() (util_gau.py:25-60).
+  ply_ref.npz       -- util_gau.load_ply (util_gau.py:63-125) itself: its activations (:114-124),
+                       f_rest reorder (:87-100), bounding box and center, on raw vertex arrays
+                       stored in the same file.  plyfile is absent, so `PlyData.read` is a shim
+                       that only hands the reference the vertex arrays and property names
+                       (oracle/ply_oracle.read_vertex, numpy's parse of the PLY written from
+                       the raw arrays); every line of load_ply after the parse is the
+                       reference's own.
 Also writes oracle_c1.npz: the oracle's integer outputs for config C1 (a regression pin of the
 restatement, NOT a reference output -- the upstream CUDA forward is not available).
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [--only ply]
 """
 from __future__ import annotations
 
@@ -62,12 +69,67 @@ def _views():
     }
 
 
-def main():
+def make_ply_ref(util_gau, tmpdir):
+    """Run the reference's load_ply on a PLY written from seeded raw arrays (float32 fields,
+    properties in a shuffled order, extreme values included) and store inputs + outputs."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import ply_oracle  # noqa: E402  (the numpy PLY parse only; the shim below feeds it)
+    rng = np.random.default_rng(77)
+    P = 1500
+    raw = {n: rng.normal(0, 1, P).astype(np.float32) for n in ("x", "y", "z", "nx", "ny", "nz")}
+    raw["x"] *= 5
+    for i in range(3):
+        raw[f"f_dc_{i}"] = rng.normal(0, 0.6, P).astype(np.float32)
+    for i in range(45):
+        raw[f"f_rest_{i}"] = rng.normal(0, 0.05, P).astype(np.float32)
+    raw["opacity"] = rng.normal(0, 4.0, P).astype(np.float32)
+    raw["opacity"][:4] = np.float32([-90.0, 90.0, 0.0, -1e-8])
+    for i in range(3):
+        raw[f"scale_{i}"] = rng.uniform(-9, 1, P).astype(np.float32)
+    for i in range(4):
+        raw[f"rot_{i}"] = rng.normal(0, 1, P).astype(np.float32)
+    raw["rot_0"][5] = np.float32(1e-20)  # tiny components
+    order = list(raw)
+    rng.shuffle(order)
+    path = os.path.join(tmpdir, "ref_input.ply")
+    ply_oracle.write_ply(path, raw, order=order)
+
+    class _Prop:
+        def __init__(self, name):
+            self.name = name
+
+    class _Element(dict):
+        pass
+
+    class _PlyData:
+        @staticmethod
+        def read(p):
+            el = _Element(ply_oracle.read_vertex(p))
+            el.properties = [_Prop(n) for n in el]
+            return types.SimpleNamespace(elements=[el])
+
+    util_gau.PlyData = _PlyData
+    g, bbox, center = util_gau.load_ply(path)
+    out = {f"raw__{n}": raw[n] for n in order}
+    out["order"] = np.array(order)
+    out.update(xyz=g.xyz, rot=g.rot, scale=g.scale, opacity=g.opacity, sh=g.sh,
+               bbox=np.asarray(bbox), center=np.asarray(center))
+    np.savez_compressed(os.path.join(HERE, "ply_ref.npz"), **out)
+
+
+def main(only=None):
     _stub_modules()
     sys.path.insert(0, REF)
     import renderer_ogl  # noqa: E402  (the reference module)
     import util  # noqa: E402
     import util_gau  # noqa: E402
+
+    if only == "ply":
+        import tempfile
+        with tempfile.TemporaryDirectory() as d:
+            make_ply_ref(util_gau, d)
+        print("wrote ply_ref.npz")
+        return
 
     assert renderer_ogl._sort_gaussian is renderer_ogl._sort_gaussian_cpu
 
@@ -132,8 +194,11 @@ def main():
                         num_rendered=np.array(r["num_rendered"]),
                         color_sum=np.array(r["color"].astype(np.float64).sum()),
                         n_contrib=r["n_contrib"])
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        make_ply_ref(util_gau, d)
     print("wrote", sorted(os.listdir(HERE)))
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None)

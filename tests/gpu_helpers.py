@@ -68,12 +68,25 @@ def ulp_diff(a, b):
     return np.abs(a - b)
 
 
-# Image tolerance: the only non-bit-exact step is expf (glibc on the host vs
-# the device's ocml expf, both faithfully rounded), which can flip a 1/255 or T<1e-4 threshold
-# in rare pixels.  Bar: >= 99.99 % of values within 1e-5, every value within 2e-2.
+# Image tolerance.  Everything before the blend is bit-exact; the blend is
+# not, for two reasons.  (1) exp: the oracle calls glibc expf, the exact mode the device's ocml
+# expf (both faithfully rounded, not always equal), and the default fast mode evaluates
+# exp2(power * log2 e) with v_exp_f32 on a conic pre-scaled by log2(e) and -1/2.  (2) FMA: fast
+# mode forms the quadratic form and T * (1 - alpha) with fused multiply-adds (T - alpha * T),
+# where the oracle rounds every product.  Both shift values by a few ulp and can flip the
+# alpha >= 1/255 or T < 1e-4 threshold of a rare pixel (one such flip moves it by <= alpha * rgb
+# ~ 1/255).  Bar: >= 99.99 % of values within 1e-5, every value within 4e-3, PSNR (peak 1)
+# >= 80 dB.  Measured at C3: 2.3e-3 max, 99.9997 % within 1e-5 (profiles/r01_blend_error_*).
 IMG_ATOL = 1e-5
 IMG_FRAC = 0.9999
-IMG_MAX = 2e-2
+IMG_MAX = 4e-3
+IMG_PSNR_DB = 80.0
+
+
+def psnr_db(got, want) -> float:
+    d = got.astype(np.float64) - want.astype(np.float64)
+    mse = float(np.mean(d * d)) if d.size else 0.0
+    return float("inf") if mse == 0.0 else 10.0 * np.log10(1.0 / mse)
 
 
 def assert_image_close(got, want, what="color"):
@@ -82,6 +95,8 @@ def assert_image_close(got, want, what="color"):
     frac = float((d <= IMG_ATOL).mean()) if d.size else 1.0
     assert frac >= IMG_FRAC, f"{what}: only {frac:.6f} of values within {IMG_ATOL}"
     assert (d.max() if d.size else 0.0) <= IMG_MAX, f"{what}: max abs diff {d.max()}"
+    p = psnr_db(got, want)
+    assert p >= IMG_PSNR_DB, f"{what}: PSNR {p:.1f} dB < {IMG_PSNR_DB} dB"
 
 
 def assert_parity(hip, orc, image=True):

@@ -123,3 +123,43 @@ def test_strip_rows_partition(gy, world):
     H = gy * 16 - 7
     covered = sum(strip_pixel_rows(r, H)[1] for r in rows)
     assert covered == H
+
+
+def test_native_entry_returns_upstream_6_tuple(monkeypatch):
+    """`_C.rasterize_gaussians` has upstream's argument order and 6-field return
+    (num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer), and GaussianRasterizer
+    reaches it through `_RasterizeGaussians` (upstream __init__.py's call chain).  The native
+    call itself is replaced here (no GPU in the CPU suite); the GPU suite runs the real one."""
+    from gaussiansplattingviewer_amd import _C, rasterizer
+    seen = {}
+
+    def fake_native(*args, **kw):
+        seen["args"] = args
+        P = args[1].shape[0]
+        H, W = args[12], args[13]
+        return rasterizer.ForwardResult(7, torch.zeros(3, H, W), torch.ones(P, dtype=torch.int32),
+                                        {})
+
+    monkeypatch.setattr(_C, "rasterize_gaussians_native", fake_native)
+    P, H, W = 5, 4, 6
+    xyz, op = torch.zeros(P, 3), torch.ones(P, 1)
+    sc, rot, sh = torch.ones(P, 3), torch.ones(P, 4), torch.zeros(P, 16, 3)
+    out = _C.rasterize_gaussians(torch.zeros(3), xyz, None, op, sc, rot, 1.0, None,
+                                 torch.eye(4), torch.eye(4), 0.5, 0.4, H, W, sh, 3,
+                                 torch.zeros(3), False, False)
+    assert len(out) == 6
+    num_rendered, color, radii, geom, binning, img = out
+    assert isinstance(num_rendered, int) and num_rendered == 7
+    assert tuple(color.shape) == (3, H, W) and color.dtype == torch.float32
+    assert tuple(radii.shape) == (P,) and radii.dtype == torch.int32
+    for b in (geom, binning, img):
+        assert isinstance(b, torch.Tensor) and b.dtype == torch.uint8
+    assert seen["args"][12:16] == (H, W, sh, 3)  # image_height, image_width, sh, sh_degree
+
+    rs = GaussianRasterizationSettings(H, W, 0.5, 0.4, torch.zeros(3), 1.0, torch.eye(4),
+                                       torch.eye(4), 3, torch.zeros(3), False, False)
+    seen.clear()
+    c2, r2 = GaussianRasterizer(rs)(means3D=xyz, means2D=None, opacities=op, shs=sh,
+                                    colors_precomp=None, scales=sc, rotations=rot,
+                                    cov3D_precomp=None)
+    assert seen["args"][1] is xyz and tuple(c2.shape) == (3, H, W)

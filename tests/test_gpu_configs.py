@@ -1,0 +1,124 @@
+"""GPU parity at the two BASELINE configs the other suites do not reach at full size.
+
+C5 (BASELINE.json configs[4]): 1M Gaussians, SH3, 1920x1080, orbit camera with a per-frame
+re-sort.  Four frames of the 1000-frame orbit (i = 0, 250, 500, 750; SURVEY.md §8(d), cf.
+main_test.py:392-426) are rendered through `FramePipeline` -- the two-frames-in-flight path the
+bench times -- and each is checked against the oracle with the full parity bar (integer outputs,
+sort order and tile ranges bit-exact; image within the SURVEY.md §8(c) tolerance).
+
+C4 (configs[3]): 6M Gaussians, SH3, 3840x2160 -- ~178M (Gaussian, tile) pairs, a 47-bit
+upstream sort key, 135 tile rows (8 bits of packed row), a 32.8k-cell difference array.  The
+full frame on one GPU is checked against the oracle, and every strip of the 8-GPU partition
+(rendered here one after another on one device, as each rank of `bench.py --gpus 8` renders
+it) is checked bit-identical to the same rows of the full frame, with its point list equal to
+the full frame's pairs of those tile rows.  The oracle frame takes ~50 s on one host core.
+"""
+import numpy as np
+import pytest
+import torch
+
+from gaussiansplattingviewer_amd.camera import orbit_eye, static_camera
+from gaussiansplattingviewer_amd.gaussian_data import synthetic_gaussians
+from gaussiansplattingviewer_amd.pipeline import FramePipeline
+from gaussiansplattingviewer_amd.rasterizer import binning_state
+from gaussiansplattingviewer_amd.strips import strip_pixel_rows, strip_rows
+
+from gpu_helpers import ALL_EXTRAS, assert_parity, run_hip, run_oracle, scene_inputs, to_dev
+from gaussiansplattingviewer_amd.rasterizer import rasterize_gaussians_native
+
+pytestmark = pytest.mark.gpu
+
+C5_FRAMES = (0, 250, 500, 750)
+
+
+@pytest.fixture(scope="module")
+def c5_scene():
+    return synthetic_gaussians(1_000_000, 3, 2)
+
+
+def _collect(res, dev, slot):
+    out = {"num_rendered": res.num_rendered, "color": res.color.cpu().numpy(),
+           "radii": res.radii.cpu().numpy()}
+    for k, v in res.extras.items():
+        out[k] = v.cpu().numpy()
+    out["tiles_touched"] = out["tiles_touched"].view(np.uint32)
+    out["n_contrib"] = out["n_contrib"].view(np.uint32)
+    pl, pt, rg = binning_state(dev.index or 0, slot=slot)
+    out["point_list"] = pl.cpu().numpy().view(np.uint32)
+    out["point_tiles"] = pt.cpu().numpy().view(np.uint32)
+    out["ranges"] = rg.cpu().numpy().view(np.uint32)
+    return out
+
+
+def test_c5_orbit_frames_through_pipeline(gpu, oracle_mod, c5_scene):
+    g = c5_scene
+    P = len(g.xyz)
+    dg = dict(xyz=to_dev(g.xyz, gpu), rot=to_dev(g.rot, gpu), scale=to_dev(g.scale, gpu),
+              opacity=to_dev(g.opacity, gpu),
+              sh=to_dev(g.sh, gpu).reshape(P, -1, 3).contiguous())
+    pipe = FramePipeline(2, gpu)
+    Ks = []
+    for i in C5_FRAMES:
+        s = scene_inputs(g, static_camera(1920, 1080, orbit_eye(i, 1000)), 3)
+        with pipe.frame() as slot:
+            res = rasterize_gaussians_native(
+                to_dev(s["bg"], gpu), dg["xyz"], None, dg["opacity"], dg["scale"], dg["rot"],
+                1.0, None, to_dev(s["view"], gpu), to_dev(s["proj"], gpu), s["tx"], s["ty"],
+                s["H"], s["W"], dg["sh"], 3, to_dev(s["campos"], gpu), False, False, slot=slot,
+                extras=ALL_EXTRAS)
+            hip = _collect(res, gpu, slot)
+        orc = run_oracle(oracle_mod, s)
+        assert orc["num_rendered"] > 5_000_000, (i, orc["num_rendered"])
+        assert_parity(hip, orc)
+        Ks.append(hip["num_rendered"])
+    pipe.synchronize()
+    assert len(set(Ks)) == len(Ks)  # the camera really moved (different binning per frame)
+
+
+@pytest.fixture(scope="module")
+def c4(oracle_mod):
+    """6M Gaussians, 3840x2160, static camera (seed 3): inputs and the oracle frame."""
+    s = scene_inputs(synthetic_gaussians(6_000_000, 3, 3), static_camera(3840, 2160), 3)
+    return s, run_oracle(oracle_mod, s)
+
+
+@pytest.fixture(scope="module")
+def c4_hip(gpu, c4):
+    s, _ = c4
+    out = run_hip(s, gpu)
+    torch.cuda.empty_cache()
+    return out
+
+
+def test_c4_full_frame_vs_oracle(c4, c4_hip):
+    s, orc = c4
+    assert orc["num_rendered"] > 100_000_000
+    # the regimes this config exists for: > 2^27 pairs, 47-bit upstream keys, 8-bit rows
+    assert int(orc["point_keys"][-1] >> np.uint64(32)) > 2 ** 14
+    assert_parity(c4_hip, orc)
+
+
+@pytest.mark.parametrize("rank", range(8))
+def test_c4_strips_equal_full_frame_rows(gpu, c4, c4_hip, rank):
+    s, _ = c4
+    full = c4_hip
+    W, H = s["W"], s["H"]
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    rows = strip_rows(gy, 8, rank)
+    part = run_hip(s, gpu, tile_rows=rows)
+    y0, n = strip_pixel_rows(rows, H)
+    np.testing.assert_array_equal(part["color"].view(np.uint32),
+                                  full["color"][:, y0:y0 + n].view(np.uint32))
+    np.testing.assert_array_equal(part["n_contrib"], full["n_contrib"][y0:y0 + n])
+    np.testing.assert_array_equal(part["final_T"].view(np.uint32),
+                                  full["final_T"][y0:y0 + n].view(np.uint32))
+    np.testing.assert_array_equal(part["radii"], full["radii"])
+    t0, t1 = rows[0] * gx, rows[1] * gx
+    lo = int(np.searchsorted(full["point_tiles"], t0))
+    hi = int(np.searchsorted(full["point_tiles"], t1))
+    assert part["num_rendered"] == hi - lo
+    np.testing.assert_array_equal(part["point_list"], full["point_list"][lo:hi])
+    np.testing.assert_array_equal(part["point_tiles"], full["point_tiles"][lo:hi])
+    nonempty = full["ranges"][t0:t1, 1] > full["ranges"][t0:t1, 0]
+    np.testing.assert_array_equal(part["ranges"][t0:t1][nonempty],
+                                  full["ranges"][t0:t1][nonempty] - lo)

@@ -113,3 +113,28 @@ def test_empty_vertex_element(tmp_path):
     ply_oracle.write_ply(p, {k: v[:0] for k, v in _raw(1, 7).items()})
     g, bbox, center = ply.load_ply(str(p))
     assert len(g) == 0 and g.sh.shape == (0, 48)
+
+
+def test_native_reader_vs_reference_captured_outputs(tmp_path, golden):
+    """Pinned to the reference itself: tests/golden/ply_ref.npz holds the outputs of
+    util_gau.load_ply (util_gau.py:63-125) -- activations, f_rest reorder, bounding box and
+    center -- captured in the build container on the raw arrays stored beside them
+    (make_golden.make_ply_ref).  The PLY is rewritten here from those arrays, in the same
+    shuffled property order, and read natively; the restated loader must agree too."""
+    z = golden("ply_ref.npz")
+    order = [str(n) for n in z["order"]]
+    raw = {n: z[f"raw__{n}"] for n in order}
+    path = tmp_path / "ref_input.ply"
+    ply_oracle.write_ply(path, raw, order=order)
+    g, bbox, center = ply.load_ply(str(path))
+    np.testing.assert_array_equal(g.xyz, z["xyz"])
+    np.testing.assert_array_equal(g.sh, z["sh"])
+    assert _ulp_diff(g.rot, z["rot"]) <= 1
+    assert _ulp_diff(g.scale, z["scale"]) <= 1
+    assert _ulp_diff(g.opacity, z["opacity"]) <= 4  # numpy SIMD exp vs libm expf
+    np.testing.assert_array_equal(bbox, z["bbox"].astype(np.float32))
+    np.testing.assert_array_equal(center, z["center"].astype(np.float32))
+    xyz, rot, scale, opac, sh, bbox_r, center_r = ply_oracle.load_ply_reference(str(path))
+    for a, b in ((xyz, "xyz"), (rot, "rot"), (scale, "scale"), (opac, "opacity"), (sh, "sh"),
+                 (bbox_r, "bbox"), (center_r, "center")):
+        np.testing.assert_array_equal(a, z[b], err_msg=b)
