@@ -62,9 +62,6 @@ def parse():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sort-shape", type=int, default=None, help="GSR_OPT_TILE_SORT_SHAPE (tuning)")
-    ap.add_argument("--depth-sort-shape", type=int, default=None,
-                    help="GSR_OPT_DEPTH_SORT_SHAPE (tuning)")
-    ap.add_argument("--onesweep", action="store_true", help="GSR_OPT_SORT_ONESWEEP (tuning)")
     ap.add_argument("--unfused", action="store_true", help="GSR_OPT_FUSED_BINNING=0 (tuning)")
     ap.add_argument("--sim-strip", default=None, metavar="R/N",
                     help="diagnostic, 1 GPU: render only strip R of an N-way partition (no "
@@ -292,8 +289,6 @@ def main():
     for c in ctxs:
         opt = lambda o, v: _lib.check(lib.gsr_set_option(c, o, v), "gsr_set_option")  # noqa: E731
         opt(_lib.GSR_OPT_BLEND_FAST, {"exact": 0, "fast": 1, "packed": 2}[args.blend])
-        if args.depth_sort_shape is not None:
-            opt(_lib.GSR_OPT_DEPTH_SORT_SHAPE, args.depth_sort_shape)
         if args.sort_shape is not None:
             opt(_lib.GSR_OPT_TILE_SORT_SHAPE, args.sort_shape)
         if args.blend_blocks:
@@ -302,8 +297,6 @@ def main():
             opt(_lib.GSR_OPT_SPLIT_COLOR, 0)
         if args.unfused:
             opt(_lib.GSR_OPT_FUSED_BINNING, 0)
-        if args.onesweep:
-            opt(_lib.GSR_OPT_SORT_ONESWEEP, 1)
 
     # Warmup (also sizes the workspace so the timed loop never allocates).
     for i in range(args.warmup):
@@ -383,8 +376,8 @@ def main():
     # flight) also count the other frame's kernels sharing the CUs; reported beside it.
     dom_ms = stage_ms[dominant]
     ach = alg[dominant] / (dom_ms * 1e-3) / 1e9
-    default_opts = not (args.sort_shape is not None or args.depth_sort_shape is not None or
-                        args.onesweep or args.unfused or args.blend_blocks or args.inline_color or
+    default_opts = not (args.sort_shape is not None or
+                        args.unfused or args.blend_blocks or args.inline_color or
                         args.blend != "fast")
     traffic, traffic_src = measured_traffic(dominant, args.config, default_opts)
     fps = args.steps / t_max

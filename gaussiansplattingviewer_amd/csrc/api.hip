@@ -44,18 +44,18 @@ const char *kStageNames[kAllStages] = {"preprocess", "depth_sort", "scan",  "dup
 struct gsr_context {
     int device = 0;
     // per-Gaussian workspace
-    DevBuf records, strip_rect, sort_keys, sort_vals, sort_keys_alt, sort_vals_alt, partials,
-        total, hist, digit_total, bin, chunk_first, rect_sorted, pair_count, valid_count;
-    // onesweep sort state: [0,1024) depth-sort digit counts, [1024,2048) tile-sort counts,
-    // then the ticket word; look-back granules
-    DevBuf sort_ctl, status;
+    DevBuf records, strip_rect, sort_keys, partials, total, hist, digit_total, bin, chunk_first,
+        rect_sorted, pair_count;
+    DevBuf ds_a, ds_b;  // depth sort: (key, id) pairs between passes (ping-pong)
+    DevBuf perm;    // the depth sort's result: Gaussian ids in depth order (kept ones)
+    DevBuf ds_ctl;  // depth sort control words: kept count, key bits, per-tile key stats
     DevBuf col_hist;  // column-first binning: per-(Gaussian block, column) pair counts
-    uint32_t epoch = 0;  // tags the look-back granules of every onesweep pass
     // per-pair workspace
     DevBuf tile_keys, tile_vals, tile_keys_alt, tile_vals_alt;
     DevBuf ranges_local;
     DevBuf tile_diff;  // difference-array partials + sum of the second-stream tile ranges
-    uint64_t *h_total = nullptr;  // pinned: [K, look-back flag, K from the preprocess]
+    // pinned: [K from the device scan (debug), unused, K from the pair count, depth key bits D]
+    uint64_t *h_total = nullptr;
     unsigned long long *d_hostK = nullptr;  // device view of h_total + 2
     hipEvent_t kcount_ready = nullptr;  // the pair counts of this frame are on the host
     // state of the last forward (for gsr_get_binning)
@@ -68,11 +68,7 @@ struct gsr_context {
     // options / timing
     int cull = 1;
     int fast = 1;
-    int onesweep = 0;
     int tile_sort_shape = 3;  // 8 waves x 8 keys/lane: fastest measured
-    // 4 waves x 4 keys (1024-key tiles): as fast as 8x8 at the full C3 frame (94 vs 92 us) and
-    // faster on strips, whose compacted sorts are small (65 vs 79 us on one of 8 strips)
-    int depth_sort_shape = 5;
     int fused_binning = 1;    // duplicate fused with the first tile-sort pass
     // tile ranges from the rects' per-tile counts on the second stream, after the colour
     // (2; 1 = before it: the colour then overlaps the duplicate stage instead of the depth
@@ -150,22 +146,23 @@ int reserve_P(gsr_context *ctx, int64_t P, hipStream_t s) {
     GSR_TRY(grow(ctx, ctx->records, n * sizeof(gsr::SplatRecord), s));
     GSR_TRY(grow(ctx, ctx->strip_rect, n * 8, s));
     GSR_TRY(grow(ctx, ctx->sort_keys, n * 4, s));
-    GSR_TRY(grow(ctx, ctx->sort_vals, n * 4, s));
-    GSR_TRY(grow(ctx, ctx->sort_keys_alt, n * 4, s));
-    GSR_TRY(grow(ctx, ctx->sort_vals_alt, n * 4, s));
+    GSR_TRY(grow(ctx, ctx->ds_a, n * 8, s));
+    GSR_TRY(grow(ctx, ctx->ds_b, n * 8, s));
     GSR_TRY(grow(ctx, ctx->partials, (size_t)std::max<int64_t>(gsr_scan_blocks(P), 1) * 4, s));
     GSR_TRY(grow_zeroed(ctx, ctx->total, 16, s));  // [K (u64), look-back error flag (u32)]
-    GSR_TRY(grow(ctx, ctx->pair_count, 8 * (size_t)((n + 255) / 256), s));  // per block
-    GSR_TRY(grow(ctx, ctx->hist, (size_t)gsr_radix_hist_words(P) * 4, s));
+    GSR_TRY(grow(ctx, ctx->pair_count, 256 * 16, s));  // k_count_pairs: 256 blocks x (8 + 8 B)
+    GSR_TRY(grow(ctx, ctx->hist, (size_t)std::max(gsr_radix_hist_words(P),
+                                                  gsr_depth_sort_hist_words(P)) * 4, s));
     // column-first binning's per-(block, column) counts: its own buffer, since reserve_K may
     // regrow hist between the count and the scatter
     GSR_TRY(grow(ctx, ctx->col_hist, (size_t)std::max<int64_t>(gsr_col_blocks(P), 1) * 256 * 4, s));
-    GSR_TRY(grow(ctx, ctx->digit_total, 256 * 4 * GSR_RADIX_MAX_PASSES, s));  // a slice / pass
-    GSR_TRY(grow(ctx, ctx->valid_count, 4, s));
+    // 256 words per radix pass; the depth sort's 4096 digits
+    GSR_TRY(grow(ctx, ctx->digit_total,
+                 (size_t)std::max(256 * GSR_RADIX_MAX_PASSES, gsr_depth_sort_digit_words()) * 4, s));
+    GSR_TRY(grow(ctx, ctx->perm, n * 4, s));
+    GSR_TRY(grow(ctx, ctx->ds_ctl, (size_t)gsr_depth_sort_ctl_words(P) * 4, s));
     GSR_TRY(grow(ctx, ctx->bin, n * 16, s));
     GSR_TRY(grow(ctx, ctx->rect_sorted, n * 8, s));
-    GSR_TRY(grow_zeroed(ctx, ctx->sort_ctl, 2048 * 4 + 256, s));
-    GSR_TRY(grow_zeroed(ctx, ctx->status, (size_t)gsr_onesweep_status_words(P) * 8, s));
     return GSR_OK;
 }
 
@@ -177,26 +174,6 @@ int reserve_K(gsr_context *ctx, int64_t K, hipStream_t s) {
     GSR_TRY(grow(ctx, ctx->tile_vals_alt, n * 4, s));
     GSR_TRY(grow(ctx, ctx->hist, (size_t)gsr_radix_hist_words(K) * 4, s));
     GSR_TRY(grow(ctx, ctx->chunk_first, (size_t)(gsr_duplicate_chunks(K) + 1) * 4, s));
-    GSR_TRY(grow_zeroed(ctx, ctx->status, (size_t)gsr_onesweep_status_words(K) * 8, s));
-    return GSR_OK;
-}
-
-GsrOnesweepWs onesweep_ws(gsr_context *ctx, int which) {
-    uint32_t *ctl = static_cast<uint32_t *>(ctx->sort_ctl.p);
-    GsrOnesweepWs ws;
-    ws.ghist = ctl + 1024 * which;
-    ws.ticket = ctl + 2048;
-    ws.err = static_cast<uint32_t *>(ctx->total.p) + 2;  // after the 64-bit K
-    ws.status = static_cast<uint64_t *>(ctx->status.p);
-    ws.epoch = &ctx->epoch;
-    return ws;
-}
-
-// Keeps the 31-bit granule epoch from wrapping into old tags: re-zero the granules first.
-int epoch_guard(gsr_context *ctx, int passes, hipStream_t s) {
-    if (ctx->epoch + (uint32_t)passes < 0x7FFFFFF0u) return GSR_OK;
-    GSR_HIP(hipMemsetAsync(ctx->status.p, 0, ctx->status.cap, s), "hipMemsetAsync(granules)");
-    ctx->epoch = 0;
     return GSR_OK;
 }
 
@@ -288,11 +265,11 @@ void gsr_destroy(gsr_context *ctx) {
     if (!ctx) return;
     (void)hipDeviceSynchronize();
     DevBuf *bufs[] = {&ctx->records,       &ctx->strip_rect,    &ctx->sort_keys,
-                      &ctx->sort_vals,     &ctx->sort_keys_alt, &ctx->sort_vals_alt,
+                      &ctx->ds_a,          &ctx->ds_b,
                       &ctx->partials,      &ctx->total,         &ctx->hist,
                       &ctx->digit_total,   &ctx->bin,           &ctx->chunk_first,
-                      &ctx->rect_sorted,   &ctx->pair_count,    &ctx->valid_count,
-                      &ctx->sort_ctl,      &ctx->status,
+                      &ctx->rect_sorted,   &ctx->pair_count,    &ctx->perm,
+                      &ctx->ds_ctl,
                       &ctx->tile_keys,     &ctx->tile_vals,
                       &ctx->tile_keys_alt, &ctx->tile_vals_alt, &ctx->ranges_local,
                       &ctx->tile_diff,     &ctx->col_hist};
@@ -343,10 +320,6 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
         ctx->fast = (int)value;
         return GSR_OK;
     }
-    if (option == GSR_OPT_SORT_ONESWEEP) {
-        ctx->onesweep = value ? 1 : 0;
-        return GSR_OK;
-    }
     if (option == GSR_OPT_BLEND_WAVE_QUADRANTS) {
         ctx->blend_wave_quadrants = value ? 1 : 0;
         return GSR_OK;
@@ -357,11 +330,6 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
     }
     if (option == GSR_OPT_FUSED_BINNING) {
         ctx->fused_binning = value ? 1 : 0;
-        return GSR_OK;
-    }
-    if (option == GSR_OPT_DEPTH_SORT_SHAPE) {
-        if (value < 0 || value > 5) return fail(GSR_E_INVALID, "gsr_set_option: shape 0..5");
-        ctx->depth_sort_shape = (int)value;
         return GSR_OK;
     }
     if (option == GSR_OPT_COLUMN_PAIRS) {
@@ -485,7 +453,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     // tile ranges on the second stream (from the rects' per-tile counts) when the strip's
     // difference array fits in LDS; else k_ranges over the sorted keys on the main stream
     const uint32_t diff_cells = gsr_tile_diff_cells(gx, rows_tiles);
-    const bool aux_ranges = ctx->split_color && !ctx->onesweep && ctx->fused_binning &&
+    const bool aux_ranges = ctx->split_color && ctx->fused_binning &&
                             ctx->aux_ranges && diff_cells <= kTileDiffMaxCells;
     if (aux_ranges)
         GSR_TRY(grow(ctx, ctx->tile_diff, (size_t)(kTileDiffBlocks + 1) * diff_cells * 4, s));
@@ -540,7 +508,6 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     pa.radii = out->radii;
     pa.records = static_cast<gsr::SplatRecord *>(ctx->records.p);
     pa.sort_keys = static_cast<uint32_t *>(ctx->sort_keys.p);
-    pa.sort_vals = static_cast<uint32_t *>(ctx->sort_vals.p);
     pa.strip_rect = static_cast<uint2 *>(ctx->strip_rect.p);
     pa.block_pairs = static_cast<uint64_t *>(ctx->pair_count.p);
     pa.host_K = ctx->d_hostK;
@@ -600,30 +567,41 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     }
     GSR_TRY(stage_end(0));
 
-    // ---- 2. stable radix sort of the Gaussians by view depth ------------------------------
-    uint32_t *dk = pa.sort_keys, *dv = pa.sort_vals;
-    uint32_t *dk_alt = static_cast<uint32_t *>(ctx->sort_keys_alt.p);
-    uint32_t *dv_alt = static_cast<uint32_t *>(ctx->sort_vals_alt.p);
+    // ---- 2. stable sort of the Gaussians by view depth (depth_sort.hip) -------------------
+    // compacting: Gaussians without pairs in the strip (sentinel keys) are dropped by the first
+    // pass; the count of the rest lands in ds_ctl[0] (device), the pass count is decided there
     uint32_t *hist = static_cast<uint32_t *>(ctx->hist.p);
     uint32_t *digit_total = static_cast<uint32_t *>(ctx->digit_total.p);
-    // sorted entries: all P (onesweep) or, compacting, the count the sort stores here
-    uint32_t *d_valid = ctx->onesweep ? nullptr : static_cast<uint32_t *>(ctx->valid_count.p);
-    if (ctx->onesweep) {
-        GSR_TRY(epoch_guard(ctx, 8, s));
-        // zero both digit-count blocks (depth + tile sort) once per frame
-        GSR_HIP(hipMemsetAsync(ctx->sort_ctl.p, 0, 2048 * 4, s), "hipMemsetAsync(digit counts)");
-        GSR_HIP(gsr_onesweep_sort(&dk, &dv, &dk_alt, &dv_alt, P, 0, 32, GSR_HIST_COUNT,
-                                  onesweep_ws(ctx, 0), s),
-                "depth sort launch");
-    } else {
-        // compacting: Gaussians without pairs in the strip (sentinel keys) are dropped by the
-        // first pass; the count of the rest lands in valid_count (device)
-        GSR_HIP(gsr_radix_sort_pairs(&dk, &dv, &dk_alt, &dv_alt, P, 0, 32, hist, digit_total, s,
-                                     ctx->depth_sort_shape, 0, d_valid),
-                "depth sort launch");
+    uint32_t *d_valid = static_cast<uint32_t *>(ctx->ds_ctl.p);
+    uint32_t *perm = static_cast<uint32_t *>(ctx->perm.p);
+    uint2 *ds_a = static_cast<uint2 *>(ctx->ds_a.p), *ds_b = static_cast<uint2 *>(ctx->ds_b.p);
+    GSR_HIP(gsr_depth_sort(pa.sort_keys, P, 1, ds_a, ds_b, perm, hist, digit_total, d_valid, 0, 1,
+                           s),
+            "depth sort launch");
+    // K (the pair count, which sizes the binning) and D (the bits in which the kept depth keys
+    // differ) come from the second stream's pair count, published in pinned memory ~10 us after
+    // the preprocess -- before pass 0 ends, so the host learns how many more passes the sort
+    // needs and queues them without idling the GPU
+    uint64_t K = 0;
+    int depth_passes = 3;
+    if (split_color) {
+        GSR_HIP(hipEventSynchronize(ctx->kcount_ready), "hipEventSynchronize(pair count)");
+        K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
+        depth_passes = gsr_depth_sort_passes((uint32_t)ctx->h_total[3]);
+    }
+    GSR_HIP(gsr_depth_sort(pa.sort_keys, P, 1, ds_a, ds_b, perm, hist, digit_total, d_valid, 1,
+                           depth_passes, s),
+            "depth sort launch");
+    if (dbg && split_color) {  // the device's own D (pass 0) must agree with the published one
+        uint32_t ctl2[2];
+        GSR_HIP(hipMemcpyAsync(ctl2, d_valid, 8, hipMemcpyDeviceToHost, s), "hipMemcpyAsync(ctl)");
+        GSR_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(ctl)");
+        if (ctl2[1] != (uint32_t)ctx->h_total[3])
+            return fail(GSR_E_HIP, "gsr_forward: depth key bits mismatch (pair count " +
+                                       std::to_string(ctx->h_total[3]) + ", sort " +
+                                       std::to_string(ctl2[1]) + ")");
     }
     GSR_TRY(stage_end(1));
-    const uint32_t *perm = dv;
 
     // ---- 3. offsets scan over depth-sorted strip tile counts; K readback --------------------
     uint32_t *partials = static_cast<uint32_t *>(ctx->partials.p);
@@ -632,7 +610,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     // column-first pair generation: packed word = strip-local tile row << col_shift | id
     const int ybits = rows_tiles > 1 ? bits_for(rows_tiles - 1) : 0;
     const int col_shift = 32 - ybits;
-    const bool colpairs = ctx->column_pairs && !ctx->onesweep && ctx->fused_binning &&
+    const bool colpairs = ctx->column_pairs && ctx->fused_binning &&
                           aux_ranges && gx <= 256 && rows_tiles <= 256 &&
                           (col_shift == 32 || (uint64_t)P <= (1ull << col_shift));
     if (colpairs) {  // per-column pair counts of the depth-sorted Gaussians + their scan
@@ -647,21 +625,14 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
                 "scan launch");
     }
     const bool check_device_total =
-        !colpairs && (ctx->onesweep || dbg || ctx->late_K || !split_color);
-    if (check_device_total)  // onesweep's look-back flag (and, in debug mode, K) from the device
+        !colpairs && (dbg || ctx->late_K || !split_color);
+    if (check_device_total)  // K from the device (debug mode: checked against the pair count)
         GSR_HIP(hipMemcpyAsync(ctx->h_total, d_total, 16, hipMemcpyDeviceToHost, s),
                 "hipMemcpyAsync(num_rendered)");
     GSR_TRY(stage_end(2));
-    uint64_t K = 0;
-    if (split_color) {
-        GSR_HIP(hipEventSynchronize(ctx->kcount_ready), "hipEventSynchronize(pair count)");
-        K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
-    }
     if (check_device_total) {
         GSR_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(num_rendered)");
         if (!split_color) K = ctx->h_total[0];
-        if (ctx->h_total[1] != 0)
-            return fail(GSR_E_HIP, "gsr_forward: radix sort look-back gave up (device flag set)");
         if (ctx->h_total[0] != K)
             return fail(GSR_E_HIP, "gsr_forward: pair count mismatch (preprocess " +
                                        std::to_string(K) + ", scan " +
@@ -681,7 +652,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     uint32_t *chunk_first = static_cast<uint32_t *>(ctx->chunk_first.p);
     hist = static_cast<uint32_t *>(ctx->hist.p);  // may have been regrown
     const GsrRadixPlan tplan = gsr_radix_plan(0, tbits);
-    const bool fused = !ctx->onesweep && ctx->fused_binning;
+    const bool fused = ctx->fused_binning != 0;
     // packed pair list: word = (tile id >> first-pass bits) << pack_shift | Gaussian id; the
     // pair keys are not stored (the ranges come from the second stream)
     const int high_bits = tplan.n == 2 ? tplan.nbits[1] : 0;
@@ -714,21 +685,14 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
             std::swap(tk, tk_alt);
             std::swap(tv, tv_alt);
         } else {
-            // the onesweep tile sort takes its digit counts from the duplicate (fused)
-            GSR_HIP(gsr_launch_duplicate(bin, chunk_first, (int64_t)K, gx, tk, tv,
-                                         ctx->onesweep ? tplan : GsrRadixPlan{},
-                                         onesweep_ws(ctx, 1).ghist, s),
+            GSR_HIP(gsr_launch_duplicate(bin, chunk_first, (int64_t)K, gx, tk, tv, s),
                     "duplicate launch");
         }
     }
     GSR_TRY(stage_end(3));
 
     // ---- 5. stable radix sort of the pairs by (strip-local) tile id -------------------------
-    if (ctx->onesweep) {
-        GSR_HIP(gsr_onesweep_sort(&tk, &tv, &tk_alt, &tv_alt, (int64_t)K, 0, tbits,
-                                  K > 0 ? GSR_HIST_READY : GSR_HIST_COUNT, onesweep_ws(ctx, 1), s),
-                "tile sort launch");
-    } else if (colpairs) {  // pass 2: the tile rows of the packed words, keys only
+    if (colpairs) {  // pass 2: the tile rows of the packed words, keys only
         uint32_t *no_vals = nullptr, *no_vals_alt = nullptr;
         if (ybits > 0)
             GSR_HIP(gsr_radix_sort_pairs(&tv, &no_vals, &tv_alt, &no_vals_alt, (int64_t)K,
@@ -864,25 +828,16 @@ int gsr_depth_argsort(gsr_context *ctx, const float *xyz, int64_t P, const float
     if (P == 0) return GSR_OK;
     GSR_TRY(reserve_P(ctx, P, s));
     uint32_t *k = static_cast<uint32_t *>(ctx->sort_keys.p);
-    uint32_t *v = static_cast<uint32_t *>(ctx->sort_vals.p);
-    uint32_t *ka = static_cast<uint32_t *>(ctx->sort_keys_alt.p);
-    uint32_t *va = static_cast<uint32_t *>(ctx->sort_vals_alt.p);
     GSR_HIP(gsr_launch_view_depth_keys(xyz, P, view_host16[8], view_host16[9], view_host16[10],
-                                       view_host16[11], k, v, out_depth, s),
+                                       view_host16[11], k, out_depth, s),
             "view depth launch");
-    if (ctx->onesweep) {
-        GSR_TRY(epoch_guard(ctx, 4, s));
-        GSR_HIP(gsr_onesweep_sort(&k, &v, &ka, &va, P, 0, 32, GSR_HIST_ZERO_AND_COUNT,
-                                  onesweep_ws(ctx, 0), s),
-                "depth argsort launch");
-    } else {
-        GSR_HIP(gsr_radix_sort_pairs(&k, &v, &ka, &va, P, 0, 32,
-                                     static_cast<uint32_t *>(ctx->hist.p),
-                                     static_cast<uint32_t *>(ctx->digit_total.p), s,
-                                     ctx->depth_sort_shape),
-                "depth argsort launch");
-    }
-    GSR_HIP(gsr_launch_index_to_i32(v, P, out_index, s), "index launch");
+    // every key is kept (no sentinel); the indices land in out_index directly (< 2^31)
+    GSR_HIP(gsr_depth_sort(k, P, 0, static_cast<uint2 *>(ctx->ds_a.p),
+                           static_cast<uint2 *>(ctx->ds_b.p), reinterpret_cast<uint32_t *>(out_index),
+                           static_cast<uint32_t *>(ctx->hist.p),
+                           static_cast<uint32_t *>(ctx->digit_total.p),
+                           static_cast<uint32_t *>(ctx->ds_ctl.p), 0, 3, s),
+            "depth argsort launch");
     return GSR_OK;
 }
 

@@ -125,8 +125,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_down(const uint32_t *__restrict
 __global__ __launch_bounds__(kBlock) void k_duplicate(
     const uint4 *__restrict__ bin, const uint32_t *__restrict__ chunk_first, uint32_t K,
     uint32_t n_chunks, uint32_t gx, uint32_t *__restrict__ tile_keys,
-    uint32_t *__restrict__ tile_vals, const GsrRadixPlan plan, uint32_t *__restrict__ ghist) {
-    __shared__ uint32_t s_hist[GSR_RADIX_MAX_PASSES][256];  // digit counts of the tile sort
+    uint32_t *__restrict__ tile_vals) {
     __shared__ uint32_t s_off[kChunk + 1];
     __shared__ uint32_t s_id[kChunk + 1];
     __shared__ uint32_t s_x0w[kChunk + 1];   // rect x0 | width << 16
@@ -137,7 +136,6 @@ __global__ __launch_bounds__(kBlock) void k_duplicate(
     const uint32_t e0 = chunk_first[c];
     const uint32_t e1 = (c + 1 < n_chunks) ? min(chunk_first[c + 1] + 1u, e_end_all) : e_end_all;
     const int ne = (int)(e1 - e0);  // <= kChunk + 1: every staged Gaussian owns >= 1 pair
-    for (int i = tid; i < GSR_RADIX_MAX_PASSES * 256; i += kBlock) (&s_hist[0][0])[i] = 0;
     for (int i = tid; i < ne; i += kBlock) {
         const uint4 b = bin[e0 + i];
         s_off[i] = b.x;
@@ -162,14 +160,6 @@ __global__ __launch_bounds__(kBlock) void k_duplicate(
         const uint32_t key = s_row0[lo] + row * gx + (x0w & 0xFFFFu) + col;
         tile_keys[o] = key;
         tile_vals[o] = s_id[lo];
-        for (int p = 0; p < plan.n; ++p)
-            atomicAdd(&s_hist[p][(key >> plan.shift[p]) & plan.mask[p]], 1u);
-    }
-    // global digit counts of the onesweep tile sort (fused: saves a pass over the keys)
-    __syncthreads();
-    for (int i = tid; i < plan.n * 256; i += kBlock) {
-        const uint32_t c = (&s_hist[0][0])[i];
-        if (c) atomicAdd(&ghist[i], c);
     }
 }
 
@@ -609,11 +599,11 @@ int64_t gsr_duplicate_chunks(int64_t K) { return (K + kChunk - 1) / kChunk; }
 
 hipError_t gsr_launch_duplicate(const uint4 *bin, const uint32_t *chunk_first, int64_t K,
                                 uint32_t gx, uint32_t *tile_keys, uint32_t *tile_vals,
-                                const GsrRadixPlan &plan, uint32_t *ghist, hipStream_t s) {
+                                hipStream_t s) {
     const int64_t nc = gsr_duplicate_chunks(K);
     if (nc == 0) return hipSuccess;
     hipLaunchKernelGGL(k_duplicate, dim3((unsigned)nc), dim3(kBlock), 0, s, bin, chunk_first,
-                       (uint32_t)K, (uint32_t)nc, gx, tile_keys, tile_vals, plan, ghist);
+                       (uint32_t)K, (uint32_t)nc, gx, tile_keys, tile_vals);
     return hipGetLastError();
 }
 

@@ -1,0 +1,444 @@
+// depth_sort.hip -- the per-frame stable sort of the Gaussians by view depth, for gfx950.
+//
+// Replaces the depth half of upstream's cub::DeviceRadixSort::SortPairs over (tile << 32 |
+// depth) keys (rasterizer_impl.cu; see DESIGN.md decision 1 for the depth-first binning) and
+// the viewer's torch / cupy / numpy argsort (renderer_ogl.py:17, :34, :51; gsr_depth_argsort).
+//
+// A wide-digit LSD radix sort that sorts only the key bits that vary:
+//   * digits of 12 bits: passes over key bits [0,12), [12,24), [24,32);
+//   * pass 0's upsweep also reduces the OR and the AND of the kept keys.  Bits where they agree
+//     are equal in every key, so only the low D = bits_for(OR ^ AND) bits need sorting: at C3
+//     every depth lies in [2, 6) (keys 0x40000000..0x40BFFFFF, D = 24) and two passes do.
+//     The forward learns D on the host with K (k_count_pairs / k_publish_K compute it on the
+//     second stream) and launches only the needed passes; callers that do not know D launch
+//     all three and the unneeded ones exit at once (the kernels read D from ctl).  The last
+//     needed pass writes the permutation straight to `perm`;
+//   * compaction: pass 0 drops the sentinel keys (0xFFFFFFFF: Gaussians without pairs in the
+//     strip) and stores the kept count on the device; later passes read it.
+// Each pass is three kernels: upsweep (per-tile 4096-bin histogram, LDS atomics), scan (per
+// digit across tiles) and downsweep.  Between passes the (key, id) pairs travel as one 8-B
+// word each.  The downsweep sorts its 4096-key tile in LDS by
+// the 12-bit digit in two stable 6-bit sub-passes (wave-ballot ranking), then writes each key
+// to digit start + tile offset + position in its digit run.  Every step keeps the tile order
+// and the order within a tile, so each pass and the sort are stable: equal depths keep the
+// Gaussian index order, as upstream's stable SortPairs does.
+#include "radix_tile.h"
+
+using namespace gsr;
+
+namespace {
+
+constexpr int kDW = 8;                  // waves per block
+constexpr int kDThreads = kDW * 64;     // 512
+constexpr int kDIt = 8;                 // keys per lane
+constexpr int kDT = kDThreads * kDIt;   // 4096 keys per tile
+constexpr int kDBits = 12;              // digit width
+constexpr int kDBins = 1 << kDBits;     // 4096
+constexpr int kDSub = 6;                // in-LDS sub-pass width
+constexpr int kDSubBins = 1 << kDSub;   // 64
+constexpr int kDPasses = 3;
+static_assert(kDSubBins * kDW == kDThreads, "one thread per (sub-digit, wave) in the rank scan");
+static_assert(kDBins == kDThreads * 8, "eight digit starts per thread in the prologue");
+
+// ctl: [0] kept count, [1] D (key bits to sort), [2..3] unused, then per tile uint4 {OR, AND,
+// kept, 0} of pass 0.
+constexpr int kCtlHead = 4;
+
+__device__ __forceinline__ int pass_bits(int shift) { return min(kDBits, 32 - shift); }
+
+// kFirst: `in` is the n keys (uint32); else the previous pass's (key, id) pairs (uint2).
+template <bool kFirst>
+__global__ __launch_bounds__(kDThreads) void k_ds_upsweep(const void *__restrict__ in,
+                                                          int64_t n_host, int drop,
+                                                          uint32_t *__restrict__ ctl, int shift,
+                                                          uint32_t *__restrict__ hist) {
+    __shared__ uint32_t s_h[kDBins];
+    __shared__ uint32_t s_red[3][kDW];
+    int64_t n = n_host;
+    if (!kFirst) {
+        if (ctl[1] <= (uint32_t)shift) return;  // constant digit: pass skipped
+        n = ctl[0];
+    }
+    const int64_t base = (int64_t)blockIdx.x * kDT;
+    if (base >= n) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nbins = 1 << pass_bits(shift);
+    const uint32_t mask = (uint32_t)nbins - 1u;
+    for (int i = tid; i < nbins; i += kDThreads) s_h[i] = 0u;
+    __syncthreads();
+    uint32_t vor = 0u, vand = 0xFFFFFFFFu, cnt = 0u;
+    auto add = [&](uint32_t k) {
+        if (kFirst && drop && k == kDropKey) return;
+        atomicAdd(&s_h[(k >> shift) & mask], 1u);
+        if (kFirst) {
+            vor |= k;
+            vand &= k;
+            ++cnt;
+        }
+    };
+    if (kFirst) {
+        const uint32_t *keys = static_cast<const uint32_t *>(in);
+        if (base + kDT <= n) {
+            const uint4 *k4 = reinterpret_cast<const uint4 *>(keys + base);
+#pragma unroll
+            for (int j = 0; j < kDIt / 4; ++j) {
+                const uint4 q = k4[j * kDThreads + tid];
+                add(q.x);
+                add(q.y);
+                add(q.z);
+                add(q.w);
+            }
+        } else {
+            for (int64_t e = base + tid; e < n; e += kDThreads) add(keys[e]);
+        }
+    } else {
+        const uint2 *pairs = static_cast<const uint2 *>(in);
+        if (base + kDT <= n) {
+            const uint4 *p4 = reinterpret_cast<const uint4 *>(pairs + base);
+#pragma unroll
+            for (int j = 0; j < kDIt / 2; ++j) {
+                const uint4 q = p4[j * kDThreads + tid];
+                add(q.x);
+                add(q.z);
+            }
+        } else {
+            for (int64_t e = base + tid; e < n; e += kDThreads) add(pairs[e].x);
+        }
+    }
+    __syncthreads();
+    uint32_t *row = hist + (int64_t)blockIdx.x * kDBins;
+    for (int i = tid; i < nbins; i += kDThreads) row[i] = s_h[i];
+    if (kFirst) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            vor |= __shfl_xor(vor, o);
+            vand &= __shfl_xor(vand, o);
+            cnt += __shfl_xor(cnt, o);
+        }
+        if (lane == 0) {
+            s_red[0][w] = vor;
+            s_red[1][w] = vand;
+            s_red[2][w] = cnt;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t o = 0u, a = 0xFFFFFFFFu, c = 0u;
+#pragma unroll
+            for (int i = 0; i < kDW; ++i) {
+                o |= s_red[0][i];
+                a &= s_red[1][i];
+                c += s_red[2][i];
+            }
+            reinterpret_cast<uint4 *>(ctl + kCtlHead)[blockIdx.x] = make_uint4(o, a, c, 0u);
+        }
+    }
+}
+
+// Block b: digits [16 b, 16 b + 16); thread t: digit 16 b + t % 16 over tile group t / 16 (a
+// sixteenth of the tiles, loaded kScanReg at a time so the loads are in flight together).
+// hist[t][d] becomes the exclusive count of digit d in tiles < t; digit_total[d] the count
+// over all tiles.  Pass 0: the last block also reduces the tiles' {OR, AND, kept} into ctl[0]
+// (kept) and ctl[1] (D).
+constexpr int kScanDigits = 16, kScanGroups = 16, kScanReg = 8;
+template <bool kFirst>
+__global__ __launch_bounds__(256) void k_ds_scan(uint32_t *__restrict__ hist, int64_t n_host,
+                                                 uint32_t *__restrict__ ctl, int shift,
+                                                 uint32_t *__restrict__ digit_total) {
+    __shared__ uint32_t s_sum[kScanGroups][kScanDigits];
+    __shared__ uint32_t s_red[3][4];
+    int64_t n = n_host;
+    if (!kFirst) {
+        if (ctl[1] <= (uint32_t)shift) return;
+        n = ctl[0];
+    }
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t nt = (uint32_t)((n + kDT - 1) / kDT);
+    const uint32_t nbins = 1u << pass_bits(shift);
+    const int dl = tid % kScanDigits, g = tid / kScanDigits;
+    const uint32_t d = blockIdx.x * kScanDigits + dl;
+    if (blockIdx.x * kScanDigits < nbins) {
+        const uint32_t t0 = (uint32_t)((uint64_t)nt * g / kScanGroups);
+        const uint32_t t1 = (uint32_t)((uint64_t)nt * (g + 1) / kScanGroups);
+        uint32_t *col = hist + d;
+        uint32_t v[kScanReg], s = 0;
+        for (uint32_t t = t0; t < t1; t += kScanReg) {
+#pragma unroll
+            for (int r = 0; r < kScanReg; ++r)
+                v[r] = t + r < t1 ? col[(int64_t)(t + r) * kDBins] : 0u;
+#pragma unroll
+            for (int r = 0; r < kScanReg; ++r) s += v[r];
+        }
+        s_sum[g][dl] = s;
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+#pragma unroll
+        for (int i = 0; i < kScanGroups; ++i) {
+            const uint32_t x = s_sum[i][dl];
+            pre += i < g ? x : 0u;
+            tot += x;
+        }
+        for (uint32_t t = t0; t < t1; t += kScanReg) {
+#pragma unroll
+            for (int r = 0; r < kScanReg; ++r)
+                v[r] = t + r < t1 ? col[(int64_t)(t + r) * kDBins] : 0u;
+#pragma unroll
+            for (int r = 0; r < kScanReg; ++r) {
+                if (t + r < t1) col[(int64_t)(t + r) * kDBins] = pre;
+                pre += v[r];
+            }
+        }
+        if (g == 0) digit_total[d] = tot;
+    }
+    if (kFirst && blockIdx.x == gridDim.x - 1) {
+        const uint4 *st = reinterpret_cast<const uint4 *>(ctl + kCtlHead);
+        uint32_t o = 0u, a = 0xFFFFFFFFu, c = 0u;
+        for (uint32_t t = tid; t < nt; t += 256) {
+            const uint4 v = st[t];
+            if (v.z) {  // tiles whose keys were all dropped carry no bits
+                o |= v.x;
+                a &= v.y;
+                c += v.z;
+            }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            o |= __shfl_xor(o, off);
+            a &= __shfl_xor(a, off);
+            c += __shfl_xor(c, off);
+        }
+        if (lane == 0) {
+            s_red[0][w] = o;
+            s_red[1][w] = a;
+            s_red[2][w] = c;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            o = 0u;
+            a = 0xFFFFFFFFu;
+            c = 0u;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                o |= s_red[0][i];
+                a &= s_red[1][i];
+                c += s_red[2][i];
+            }
+            const uint32_t diff = c ? (o ^ a) : 0u;
+            ctl[0] = c;
+            ctl[1] = diff ? 32u - (uint32_t)__clz(diff) : 0u;
+        }
+    }
+}
+
+// Stable rank of the tile's kept elements by kBits key bits at `shift` and scatter into
+// s_keys / s_vals in that order (element order: wave, then item, then lane).  Returns the
+// number of kept elements.  s_wcnt: kDW x kDSubBins counters, index wave * 64 + digit (distinct
+// digits of a wave hit distinct banks).
+//
+// Per item, each lane finds the lanes of its wave holding its digit with one ballot per bit:
+// m &= ~(ballot(bit) ^ f), f = the lane's own bit sign-extended to a full mask (one v_bitop3
+// per 32-bit half); its rank is the count of those lanes below it, and every matching lane
+// stores the same new running count.
+template <int kBits>
+__device__ __forceinline__ int tile_rank_scatter(const uint32_t (&k)[kDIt],
+                                                 const uint32_t (&v)[kDIt], uint32_t keep,
+                                                 int shift, uint32_t *s_keys, uint32_t *s_vals,
+                                                 uint32_t *s_wcnt, uint32_t *s_tmp) {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    constexpr uint32_t kMask = (1u << kBits) - 1u;
+    s_wcnt[tid] = 0u;
+    __syncthreads();
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t *wcnt = s_wcnt + w * kDSubBins;
+    uint32_t rank[kDIt];
+#pragma unroll
+    for (int j = 0; j < kDIt; ++j) {
+        const bool kp = (keep >> j) & 1u;
+        const uint32_t d = (k[j] >> shift) & kMask;
+        const uint64_t m0 = __ballot(kp);
+        uint32_t mlo = (uint32_t)m0, mhi = (uint32_t)(m0 >> 32);
+#pragma unroll
+        for (int b = 0; b < kBits; ++b) {
+            const uint32_t f = (uint32_t)(((int32_t)(d << (31 - b))) >> 31);
+            const uint64_t bal = __ballot(f != 0u);
+            mlo &= ~((uint32_t)bal ^ f);
+            mhi &= ~((uint32_t)(bal >> 32) ^ f);
+        }
+        const uint64_t m = ((uint64_t)mhi << 32) | mlo;
+        const uint32_t prior = wcnt[d];
+        rank[j] = prior + (uint32_t)__popcll(m & lt);
+        if (kp) wcnt[d] = prior + (uint32_t)__popcll(m);  // same value from every match
+    }
+    __syncthreads();
+    // exclusive scan in (digit, wave) order: thread t = digit * kDW + wave
+    const int sd = tid / kDW, sw = tid % kDW;
+    uint32_t total;
+    const uint32_t c = s_wcnt[sw * kDSubBins + sd];
+    const uint32_t pre = blockw_exclusive_scan<kDW>(c, s_tmp, total);
+    s_wcnt[sw * kDSubBins + sd] = pre;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kDIt; ++j) {
+        if (!((keep >> j) & 1u)) continue;
+        const uint32_t d = (k[j] >> shift) & kMask;
+        const uint32_t pos = wcnt[d] + rank[j];
+        s_keys[pos] = k[j];
+        s_vals[pos] = v[j];
+    }
+    __syncthreads();
+    return (int)total;
+}
+
+// kFirst: `in` is the n keys and the values are the element indices; else `in` is the
+// previous pass's (key, id) pairs.  last (decided from D on the device): write only the ids,
+// to perm; else the (key, id) pairs to pairs_out.
+template <bool kFirst>
+__global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
+    const void *__restrict__ in, uint2 *__restrict__ pairs_out, uint32_t *__restrict__ perm,
+    int64_t n_host, int drop, const uint32_t *__restrict__ ctl, int shift,
+    const uint32_t *__restrict__ hist, const uint32_t *__restrict__ digit_total) {
+    __shared__ uint32_t s_keys[kDT], s_vals[kDT], s_tab[kDBins];  // 48 KiB
+    __shared__ uint32_t s_wcnt[kDSubBins * kDW];
+    __shared__ uint32_t s_tmp[kDW];
+    const uint32_t D = ctl[1];
+    int64_t n = n_host;
+    if (!kFirst) {
+        if (D <= (uint32_t)shift) return;
+        n = ctl[0];
+    }
+    const int64_t base = (int64_t)blockIdx.x * kDT;
+    if (base >= n) return;
+    const int nbits = pass_bits(shift);
+    const bool last = shift + nbits >= 32 || D <= (uint32_t)(shift + nbits);
+    const uint32_t nbins = 1u << nbits, mask = nbins - 1u;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+
+    uint32_t k[kDIt], v[kDIt], keep = 0u;
+#pragma unroll
+    for (int j = 0; j < kDIt; ++j) {
+        const int64_t e = base + w * (kDT / kDW) + j * 64 + lane;
+        const bool valid = e < n;
+        if (kFirst) {
+            k[j] = valid ? static_cast<const uint32_t *>(in)[e] : 0u;
+            v[j] = (uint32_t)e;
+        } else {
+            const uint2 q = valid ? static_cast<const uint2 *>(in)[e] : make_uint2(0u, 0u);
+            k[j] = q.x;
+            v[j] = q.y;
+        }
+        if (valid && !(kFirst && drop && k[j] == kDropKey)) keep |= 1u << j;
+    }
+    // s_tab[d] = start of digit d overall + its count in earlier tiles (8 digits per thread:
+    // the exclusive scan of the digit totals plus this tile's row of the scanned histogram)
+    {
+        const uint32_t d0 = (uint32_t)tid * 8;
+        uint32_t c[8], h[8], sum = 0;
+        if (d0 < nbins) {
+            const uint4 *t4 = reinterpret_cast<const uint4 *>(digit_total + d0);
+            const uint4 *h4 =
+                reinterpret_cast<const uint4 *>(hist + (int64_t)blockIdx.x * kDBins + d0);
+            const uint4 ta = t4[0], tb = t4[1], ha = h4[0], hb = h4[1];
+            c[0] = ta.x; c[1] = ta.y; c[2] = ta.z; c[3] = ta.w;
+            c[4] = tb.x; c[5] = tb.y; c[6] = tb.z; c[7] = tb.w;
+            h[0] = ha.x; h[1] = ha.y; h[2] = ha.z; h[3] = ha.w;
+            h[4] = hb.x; h[5] = hb.y; h[6] = hb.z; h[7] = hb.w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) c[i] = h[i] = 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sum += c[i];
+        uint32_t tot;
+        uint32_t pre = blockw_exclusive_scan<kDW>(sum, s_tmp, tot);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            s_tab[d0 + i] = pre + h[i];
+            pre += c[i];
+        }
+    }
+    // every pass has >= 8 bits: sub-pass A takes 6, sub-pass B the remaining 6 or 2
+    int kept = tile_rank_scatter<kDSub>(k, v, keep, shift, s_keys, s_vals, s_wcnt, s_tmp);
+#ifdef GSR_DS_PROBE_NO_SUB_B
+    if (false) {
+#else
+    if (nbits > kDSub) {
+#endif
+        keep = 0u;
+#pragma unroll
+        for (int j = 0; j < kDIt; ++j) {
+            const int p = w * (kDT / kDW) + j * 64 + lane;
+            if (p < kept) {
+                k[j] = s_keys[p];
+                v[j] = s_vals[p];
+                keep |= 1u << j;
+            }
+        }
+        __syncthreads();  // every lane holds its elements before the LDS is overwritten
+        kept = nbits - kDSub == kDSub
+                   ? tile_rank_scatter<kDSub>(k, v, keep, shift + kDSub, s_keys, s_vals, s_wcnt,
+                                              s_tmp)
+                   : tile_rank_scatter<2>(k, v, keep, shift + kDSub, s_keys, s_vals, s_wcnt,
+                                          s_tmp);
+    }
+    // s_tab[d] <- global position of the tile's first digit-d key, minus its tile position
+    for (int i = tid; i < kept; i += kDThreads) {
+        const uint32_t d = (s_keys[i] >> shift) & mask;
+        if (i == 0 || ((s_keys[i - 1] >> shift) & mask) != d) s_tab[d] -= (uint32_t)i;
+    }
+    __syncthreads();
+#ifdef GSR_DS_PROBE_NO_STORE  // tools/micro/ds_probe.hip: timing without the output stores
+    if (kept > 0) return;
+#endif
+    for (int i = tid; i < kept; i += kDThreads) {
+        const uint32_t kk = s_keys[i];
+        const uint32_t g = s_tab[(kk >> shift) & mask] + (uint32_t)i;
+        if (last)
+            perm[g] = s_vals[i];
+        else
+            pairs_out[g] = make_uint2(kk, s_vals[i]);
+    }
+}
+
+}  // namespace
+
+int64_t gsr_depth_sort_hist_words(int64_t n) {
+    const int64_t nt = (n + kDT - 1) / kDT;
+    return (nt < 1 ? 1 : nt) * kDBins;
+}
+
+int64_t gsr_depth_sort_ctl_words(int64_t n) { return kCtlHead + 4 * ((n + kDT - 1) / kDT + 1); }
+
+int gsr_depth_sort_digit_words() { return kDBins; }
+
+int gsr_depth_sort_passes(uint32_t key_bits) {
+    return key_bits <= (uint32_t)kDBits ? 1 : key_bits <= (uint32_t)(2 * kDBits) ? 2 : kDPasses;
+}
+
+hipError_t gsr_depth_sort(const uint32_t *keys, int64_t n, int drop, uint2 *pairs_a,
+                          uint2 *pairs_b, uint32_t *perm, uint32_t *hist, uint32_t *digit_total,
+                          uint32_t *ctl, int pass_begin, int pass_end, hipStream_t s) {
+    if (n <= 0 || pass_begin >= pass_end) return hipSuccess;
+    if (n > (int64_t)UINT32_MAX || pass_begin < 0 || pass_end > kDPasses)
+        return hipErrorInvalidValue;
+    const unsigned nt = (unsigned)((n + kDT - 1) / kDT);
+    const void *in[kDPasses] = {keys, pairs_a, pairs_b};
+    uint2 *out[kDPasses] = {pairs_a, pairs_b, nullptr};
+    for (int p = pass_begin; p < pass_end; ++p) {
+        const int shift = p * kDBits;
+        if (p == 0) {
+            hipLaunchKernelGGL(k_ds_upsweep<true>, dim3(nt), dim3(kDThreads), 0, s, in[p], n, drop,
+                               ctl, shift, hist);
+            hipLaunchKernelGGL(k_ds_scan<true>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist,
+                               n, ctl, shift, digit_total);
+            hipLaunchKernelGGL(k_ds_downsweep<true>, dim3(nt), dim3(kDThreads), 0, s, in[p], out[p],
+                               perm, n, drop, ctl, shift, hist, digit_total);
+        } else {
+            hipLaunchKernelGGL(k_ds_upsweep<false>, dim3(nt), dim3(kDThreads), 0, s, in[p], n, 0,
+                               ctl, shift, hist);
+            hipLaunchKernelGGL(k_ds_scan<false>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist,
+                               n, ctl, shift, digit_total);
+            hipLaunchKernelGGL(k_ds_downsweep<false>, dim3(nt), dim3(kDThreads), 0, s, in[p],
+                               out[p], perm, n, 0, ctl, shift, hist, digit_total);
+        }
+    }
+    return hipGetLastError();
+}

@@ -209,12 +209,14 @@ struct GsrPreprocessArgs {
     // workspace outputs
     int32_t *radii;
     gsr::SplatRecord *records;
-    uint32_t *sort_keys, *sort_vals;
+    uint32_t *sort_keys;  // depth keys (0xFFFFFFFF: no pair in the strip); values are indices
     // per Gaussian: strip-clipped tile rect {x0 | width << 16, strip-local row0 | rows << 16},
     // {0, 0} when it has no pair in the strip (grid dimensions < 2^16, checked by the host)
     uint2 *strip_rect;
-    uint64_t *block_pairs;  // per k_count_pairs block: its (Gaussian, strip tile) pair count
-    unsigned long long *host_K;  // pinned host memory (device-mapped): K of this frame
+    // per k_count_pairs block (256): its (Gaussian, strip tile) pair count, then 256 uint2 of
+    // the OR / AND of its kept depth keys
+    uint64_t *block_pairs;
+    unsigned long long *host_K;  // pinned host memory (device-mapped): [K, D] of this frame
     // optional debug outputs
     float *depths, *means2D, *conic_opacity, *rgb;
     uint32_t *tiles_touched;
@@ -230,8 +232,7 @@ hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s);
 hipError_t gsr_launch_mark_visible(const float *means3D, int64_t P, const float *viewmatrix,
                                    uint8_t *visible, hipStream_t s);
 hipError_t gsr_launch_view_depth_keys(const float *xyz, int64_t P, float v20, float v21, float v22,
-                                      float v23, uint32_t *keys, uint32_t *vals, float *depth_out,
-                                      hipStream_t s);
+                                      float v23, uint32_t *keys, float *depth_out, hipStream_t s);
 hipError_t gsr_launch_index_to_i32(const uint32_t *vals, int64_t P, int32_t *out, hipStream_t s);
 
 // Radix sort of (uint32 key, uint32 value) pairs, stable, LSD over key bits [begin, end).
@@ -251,10 +252,7 @@ hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **key
 hipError_t gsr_launch_digit_scan(uint32_t *hist, int64_t nb, uint32_t *digit_total,
                                  hipStream_t s);
 
-// Onesweep radix sort (one kernel per pass, decoupled look-back).  Pass plan: the key bits
-// [begin, end) split into n <= 4 passes of <= 8 bits.  ghist holds the global digit counts of
-// every pass ([pass][256]); hist_ready = the caller already accumulated them (fused into the
-// kernel that produced the keys, e.g. k_duplicate) -- see hist_state.
+// Radix pass plan: the key bits [begin, end) split into n <= 4 passes of <= 8 bits.
 #define GSR_RADIX_MAX_PASSES 4
 struct GsrRadixPlan {
     int n;
@@ -262,19 +260,24 @@ struct GsrRadixPlan {
     int nbits[GSR_RADIX_MAX_PASSES];
     uint32_t mask[GSR_RADIX_MAX_PASSES];
 };
-struct GsrOnesweepWs {
-    uint32_t *ghist;   // [GSR_RADIX_MAX_PASSES][256]
-    uint64_t *status;  // gsr_onesweep_status_words(n) granules, zero-initialised once
-    uint32_t *ticket;  // one word, zero-initialised once (rewound by every pass)
-    uint32_t *err;     // look-back give-up flag
-    uint32_t *epoch;   // HOST counter, tags every pass's granules
-};
 GsrRadixPlan gsr_radix_plan(int begin_bit, int end_bit);
-int64_t gsr_onesweep_status_words(int64_t n);
-enum { GSR_HIST_ZERO_AND_COUNT = 0, GSR_HIST_COUNT = 1, GSR_HIST_READY = 2 };
-hipError_t gsr_onesweep_sort(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
-                             uint32_t **vals_alt, int64_t n, int begin_bit, int end_bit,
-                             int hist_state, const GsrOnesweepWs &ws, hipStream_t s);
+
+// Depth sort (depth_sort.hip): stable sort of n 32-bit keys, values = indices, in passes of
+// 12 key bits (pass p: bits [12p, 12p + 12)).  drop: keys 0xFFFFFFFF are dropped; the kept
+// count lands in ctl[0] and the bits in which the kept keys differ (D) in ctl[1], both on the
+// device after pass 0.  Passes [pass_begin, pass_end) are launched; a pass with 12p >= D exits
+// at once and the last needed pass writes the permutation (ids of the kept keys in key order)
+// to perm.  A caller that knows D launches gsr_depth_sort_passes(D) passes in total, else all
+// three.  pairs_a / pairs_b: n (key, id) pairs each (ping-pong scratch); hist:
+// gsr_depth_sort_hist_words(n), digit_total: gsr_depth_sort_digit_words(), ctl:
+// gsr_depth_sort_ctl_words(n) words.
+int64_t gsr_depth_sort_hist_words(int64_t n);
+int64_t gsr_depth_sort_ctl_words(int64_t n);
+int gsr_depth_sort_digit_words();
+int gsr_depth_sort_passes(uint32_t key_bits);
+hipError_t gsr_depth_sort(const uint32_t *keys, int64_t n, int drop, uint2 *pairs_a,
+                          uint2 *pairs_b, uint32_t *perm, uint32_t *hist, uint32_t *digit_total,
+                          uint32_t *ctl, int pass_begin, int pass_end, hipStream_t s);
 
 // Binning: offsets scan over depth-sorted strip tile counts, duplicate into (tile, id)
 // pairs, and tile ranges.
@@ -295,7 +298,7 @@ hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint2 *rect_sorted,
 int64_t gsr_duplicate_chunks(int64_t K);
 hipError_t gsr_launch_duplicate(const uint4 *bin, const uint32_t *chunk_first, int64_t K,
                                 uint32_t gx, uint32_t *tile_keys, uint32_t *tile_vals,
-                                const GsrRadixPlan &plan, uint32_t *ghist, hipStream_t s);
+                                hipStream_t s);
 // Fused duplicate + first tile-sort radix pass (digit (key >> shift) & (2^nbits - 1)):
 // writes the K pairs, stably ordered by that digit, to keys_out / vals_out.  Uses
 // chunk_first as written by gsr_launch_scan_down; hist needs gsr_radix_hist_words(K) words.

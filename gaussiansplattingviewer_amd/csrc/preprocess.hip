@@ -231,8 +231,7 @@ __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, i
     }
     a.radii[idx] = radius_out;
     a.strip_rect[idx] = strip_rect;
-    a.sort_keys[idx] = key;
-    a.sort_vals[idx] = (uint32_t)idx;
+    a.sort_keys[idx] = key;  // the depth sort's values are the indices (implicit)
     if (a.tiles_touched) a.tiles_touched[idx] = strip_tiles;
     return strip_tiles;
 }
@@ -245,21 +244,46 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
 }
 
 // One block, after k_count_pairs on the second stream (the kernel boundary makes its stores
-// visible): K = sum of the per-block pair counts, stored straight into pinned host memory
-// (system scope) so the host can read it as soon as this kernel's completion event fires --
-// no copy, and nothing added to the main stream.
+// visible): K = sum of the per-block pair counts and D = the bits in which the kept depth keys
+// differ (bits of OR ^ AND: the depth sort's pass count), stored straight into pinned host
+// memory (system scope) so the host can read them as soon as this kernel's completion event
+// fires -- no copy, and nothing added to the main stream.  host_K[0] = K, host_K[1] = D.
 __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__restrict__ cnt,
-                                                    int64_t n, unsigned long long *host_K) {
+                                                    const uint2 *__restrict__ keybits, int64_t n,
+                                                    unsigned long long *host_K) {
     __shared__ unsigned long long s_w[16];
+    __shared__ uint32_t s_or[16], s_and[16];
     unsigned long long v = 0;
-    for (int64_t i = threadIdx.x; i < n; i += 1024) v += cnt[i];
+    uint32_t o = 0u, a = 0xFFFFFFFFu;
+    for (int64_t i = threadIdx.x; i < n; i += 1024) {
+        v += cnt[i];
+        o |= keybits[i].x;
+        a &= keybits[i].y;
+    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+    for (int off = 32; off > 0; off >>= 1) {
+        v += __shfl_xor(v, off);
+        o |= __shfl_xor(o, off);
+        a &= __shfl_xor(a, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_w[threadIdx.x >> 6] = v;
+        s_or[threadIdx.x >> 6] = o;
+        s_and[threadIdx.x >> 6] = a;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long t = 0;
-        for (int i = 0; i < 16; ++i) t += s_w[i];
+        o = 0u;
+        a = 0xFFFFFFFFu;
+        for (int i = 0; i < 16; ++i) {
+            t += s_w[i];
+            o |= s_or[i];
+            a &= s_and[i];
+        }
+        const uint32_t diff = t ? (o ^ a) : 0u;
+        const unsigned long long D = diff ? 32u - (uint32_t)__clz(diff) : 0u;
+        __hip_atomic_store(host_K + 1, D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(host_K, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -351,23 +375,45 @@ __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
     }
 }
 
-// K for the host, on the second stream right after the preprocess: per-block sums of the
-// (Gaussian, strip tile) pair counts from the packed strip rects (grid-stride, 256 blocks).
+// K and the depth keys' bit span for the host, on the second stream right after the
+// preprocess: per-block sums of the (Gaussian, strip tile) pair counts from the packed strip
+// rects, and the OR / AND of the depth keys of the Gaussians with pairs (the sort keys the
+// depth sort keeps), grid-stride over 256 blocks.
 constexpr int kCountBlocks = 256;
 __global__ __launch_bounds__(256) void k_count_pairs(const uint2 *__restrict__ strip_rect,
-                                                     int64_t P,
-                                                     unsigned long long *__restrict__ block_pairs) {
+                                                     const uint32_t *__restrict__ keys, int64_t P,
+                                                     unsigned long long *__restrict__ block_pairs,
+                                                     uint2 *__restrict__ block_keybits) {
     unsigned long long v = 0;
+    uint32_t o = 0u, a = 0xFFFFFFFFu;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P; i += (int64_t)gridDim.x * 256) {
         const uint2 r = strip_rect[i];
         v += (unsigned long long)((r.x >> 16) * (r.y >> 16));
+        if (r.x != 0u) {  // has pairs in the strip <=> its depth key is kept
+            const uint32_t k = keys[i];
+            o |= k;
+            a &= k;
+        }
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    for (int off = 32; off > 0; off >>= 1) {
+        v += __shfl_xor(v, off);
+        o |= __shfl_xor(o, off);
+        a &= __shfl_xor(a, off);
+    }
     __shared__ unsigned long long s_w[4];
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+    __shared__ uint32_t s_or[4], s_and[4];
+    if ((threadIdx.x & 63) == 0) {
+        s_w[threadIdx.x >> 6] = v;
+        s_or[threadIdx.x >> 6] = o;
+        s_and[threadIdx.x >> 6] = a;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) block_pairs[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    if (threadIdx.x == 0) {
+        block_pairs[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        block_keybits[blockIdx.x] = make_uint2(s_or[0] | s_or[1] | s_or[2] | s_or[3],
+                                               s_and[0] & s_and[1] & s_and[2] & s_and[3]);
+    }
 }
 
 // GaussianRasterizer.markVisible -> upstream markVisible kernel: in_frustum only.
@@ -386,14 +432,12 @@ __global__ __launch_bounds__(256) void k_mark_visible(const float *__restrict__ 
 // uint32 key so the stable radix sort returns np.argsort(depth, kind='stable').
 __global__ __launch_bounds__(256) void k_view_depth_keys(const float *__restrict__ xyz, int64_t P,
                                                          float v20, float v21, float v22, float v23,
-                                                         uint32_t *keys, uint32_t *vals,
-                                                         float *depth_out) {
+                                                         uint32_t *keys, float *depth_out) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= P) return;
     const float x = xyz[3 * idx], y = xyz[3 * idx + 1], z = xyz[3 * idx + 2];
     const float d = __builtin_fmaf(v22, z, __builtin_fmaf(v20, x, v21 * y)) + v23;
     keys[idx] = float_sort_key(d);
-    vals[idx] = (uint32_t)idx;
     if (depth_out) depth_out[idx] = d;
 }
 
@@ -428,11 +472,12 @@ hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, hipStrea
 hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s) {
     if (a.P == 0) return hipSuccess;
     const unsigned g = std::min<unsigned>(kCountBlocks, grid_for(a.P));
-    hipLaunchKernelGGL(k_count_pairs, dim3(g), dim3(256), 0, s, a.strip_rect, a.P,
-                       reinterpret_cast<unsigned long long *>(a.block_pairs));
+    uint2 *keybits = reinterpret_cast<uint2 *>(a.block_pairs + kCountBlocks);
+    hipLaunchKernelGGL(k_count_pairs, dim3(g), dim3(256), 0, s, a.strip_rect, a.sort_keys, a.P,
+                       reinterpret_cast<unsigned long long *>(a.block_pairs), keybits);
     hipLaunchKernelGGL(k_publish_K, dim3(1), dim3(1024), 0, s,
-                       reinterpret_cast<const unsigned long long *>(a.block_pairs), (int64_t)g,
-                       a.host_K);
+                       reinterpret_cast<const unsigned long long *>(a.block_pairs), keybits,
+                       (int64_t)g, a.host_K);
     return hipGetLastError();
 }
 
@@ -445,11 +490,10 @@ hipError_t gsr_launch_mark_visible(const float *means3D, int64_t P, const float 
 }
 
 hipError_t gsr_launch_view_depth_keys(const float *xyz, int64_t P, float v20, float v21, float v22,
-                                      float v23, uint32_t *keys, uint32_t *vals, float *depth_out,
-                                      hipStream_t s) {
+                                      float v23, uint32_t *keys, float *depth_out, hipStream_t s) {
     if (P == 0) return hipSuccess;
     hipLaunchKernelGGL(k_view_depth_keys, dim3(grid_for(P)), dim3(256), 0, s, xyz, P, v20, v21,
-                       v22, v23, keys, vals, depth_out);
+                       v22, v23, keys, depth_out);
     return hipGetLastError();
 }
 

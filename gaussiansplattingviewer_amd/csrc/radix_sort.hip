@@ -5,19 +5,7 @@
 // (renderer_ogl.py:17, :34, :51).  Used twice per frame: Gaussians by depth (32-bit keys)
 // and (Gaussian, tile) pairs by tile id (ceil(log2 T) bits).
 //
-// Two implementations, same results (tested against each other and against numpy):
-//
-// ONESWEEP (default, gsr_onesweep_sort): one global digit histogram for all passes up front
-// (k_rs_hist, or fused into the producer of the keys), then ONE kernel per pass.  Tiles take a
-// ticket (atomic counter) so tile t only waits on tiles < t, which already run; each tile
-// publishes its per-digit count and then its inclusive prefix as self-tagged 8-byte granules
-// ({epoch<<1|inclusive, value}, one relaxed agent-scope atomic store each -- the
-// "data is the flag" hand-off of cdna_hip_programming.md Guideline 16 R2) and finds its
-// exclusive prefix by decoupled look-back over its predecessors' granules.  A pass therefore
-// reads and writes every pair once.  Passes carry <= 8 bits, split evenly (13 bits -> 7 + 6,
-// so each digit run in a 4096-pair tile averages 32 pairs = 128-B stores).
-//
-// REDUCE-THEN-SCAN (gsr_radix_sort_pairs): one pass per 8-bit digit, three kernels per pass:
+// Reduce-then-scan (gsr_radix_sort_pairs): one pass per 8-bit digit, three kernels per pass:
 //   upsweep   -- per-tile digit histogram (tile = 4096 elements = 256 threads x 16);
 //   scan      -- per digit, exclusive scan of its histogram column across tiles;
 //   downsweep -- wave-ballot ranking: each wave resolves the lanes that share its digit with
@@ -173,150 +161,6 @@ __global__ __launch_bounds__(kW * 64) void k_rs_downsweep(
                                        s_vals);
 }
 
-// ---- onesweep -----------------------------------------------------------------------------
-
-// Global digit counts of every pass (plan.n passes of <= 8 bits), grid-stride.
-__global__ __launch_bounds__(kBlock) void k_rs_hist(const uint32_t *__restrict__ keys, int64_t n,
-                                                    const GsrRadixPlan plan,
-                                                    uint32_t *__restrict__ ghist) {
-    __shared__ uint32_t s_h[GSR_RADIX_MAX_PASSES][kRadix];
-    const int tid = threadIdx.x;
-    for (int i = tid; i < GSR_RADIX_MAX_PASSES * kRadix; i += kBlock) (&s_h[0][0])[i] = 0;
-    __syncthreads();
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t e = (int64_t)blockIdx.x * kBlock + tid; e < n; e += stride) {
-        const uint32_t k = keys[e];
-        for (int p = 0; p < plan.n; ++p)
-            atomicAdd(&s_h[p][(k >> plan.shift[p]) & plan.mask[p]], 1u);
-    }
-    __syncthreads();
-    for (int i = tid; i < plan.n * kRadix; i += kBlock) {
-        const uint32_t c = (&s_h[0][0])[i];
-        if (c) atomicAdd(&ghist[i], c);
-    }
-}
-
-__device__ __forceinline__ void store_granule(uint64_t *g, uint32_t tag, uint32_t value) {
-    __hip_atomic_store(g, ((uint64_t)tag << 32) | value, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int kIt>
-__global__ __launch_bounds__(kBlock) void k_rs_onesweep(
-    const uint32_t *__restrict__ keys_in, const uint32_t *__restrict__ vals_in,
-    uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out, int64_t n, int shift,
-    int nbits, const uint32_t *__restrict__ ghist, uint64_t *__restrict__ status,
-    uint32_t *__restrict__ ticket, uint32_t epoch, uint32_t *__restrict__ err) {
-    constexpr int kT = kBlock * kIt;
-    __shared__ uint32_t s_keys[kT];
-    __shared__ uint32_t s_vals[kT];
-    __shared__ uint32_t s_wcnt[4][kRadix];
-    __shared__ uint32_t s_delta[kRadix];
-    __shared__ uint32_t s_tmp[8];
-    __shared__ uint32_t s_tile;
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const uint32_t mask = (1u << nbits) - 1u;
-    const uint32_t nb = (uint32_t)((n + kT - 1) / kT);
-    if (tid == 0) {
-        const uint32_t t = atomicAdd(ticket, 1u);
-        // the last ticket: every block has taken its ticket, so the counter can be rewound
-        // for the next pass (kernels on one stream do not overlap)
-        if (t == nb - 1) atomicExch(ticket, 0u);
-        s_tile = t;
-    }
-    for (int i = tid; i < 4 * kRadix; i += kBlock) (&s_wcnt[0][0])[i] = 0;
-    __syncthreads();
-    const uint32_t b = s_tile;
-
-    const int64_t base = (int64_t)b * kT;
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint32_t k[kIt], v[kIt], rank[kIt];
-#pragma unroll
-    for (int j = 0; j < kIt; ++j) {
-        const int64_t e = base + w * (kT / 4) + j * 64 + lane;
-        const bool valid = e < n;
-        k[j] = valid ? keys_in[e] : 0xFFFFFFFFu;  // tail -> largest digit, after every real key
-        v[j] = valid ? vals_in[e] : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < kIt; ++j) {
-        const uint32_t d = (k[j] >> shift) & mask;
-        uint64_t m = ~0ull;
-        for (int bit_i = 0; bit_i < nbits; ++bit_i) {
-            const bool bit = (d >> bit_i) & 1u;
-            const uint64_t bal = __ballot(bit);
-            m &= bit ? bal : ~bal;
-        }
-        const uint32_t prior = s_wcnt[w][d];
-        rank[j] = prior + (uint32_t)__popcll(m & lt_mask);
-        if (lane == 63 - __clzll(m)) s_wcnt[w][d] = prior + (uint32_t)__popcll(m);
-    }
-    __syncthreads();
-
-    {
-        const int d = tid;
-        const uint32_t c0 = s_wcnt[0][d], c1 = s_wcnt[1][d], c2 = s_wcnt[2][d], c3 = s_wcnt[3][d];
-        // the tail's sentinel keys (largest digit) are not part of the data
-        const int64_t rem = n - base;
-        const uint32_t pad = rem < kT ? (uint32_t)(kT - rem) : 0u;
-        const uint32_t cnt = c0 + c1 + c2 + c3 - (d == (int)mask ? pad : 0u);
-        uint32_t tile_total, all_total;
-        const uint32_t local_start = block256_exclusive_scan(c0 + c1 + c2 + c3, s_tmp, tile_total);
-        const uint32_t digit_start = block256_exclusive_scan(ghist[d], s_tmp + 4, all_total);
-        uint32_t prefix = 0;
-        if (d <= (int)mask) {
-            uint64_t *mine = status + (uint64_t)b * kRadix + d;
-            if (b == 0) {
-                store_granule(mine, (epoch << 1) | 1u, cnt);
-            } else {
-                store_granule(mine, epoch << 1, cnt);
-                // decoupled look-back over the predecessors' granules
-                int64_t j = (int64_t)b - 1;
-                uint32_t spins = 0;
-                while (true) {
-                    const uint64_t g = __hip_atomic_load(status + (uint64_t)j * kRadix + d,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t tag = (uint32_t)(g >> 32);
-                    if ((tag >> 1) == epoch) {
-                        prefix += (uint32_t)g;
-                        if ((tag & 1u) || j == 0) break;
-                        --j;
-                    } else {
-                        if (++spins > (1u << 24)) {  // bounded: flag and give up
-                            atomicOr(err, 1u);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                }
-                store_granule(mine, (epoch << 1) | 1u, prefix + cnt);
-            }
-        }
-        s_delta[d] = digit_start + prefix - local_start;
-        s_wcnt[0][d] = local_start;
-        s_wcnt[1][d] = local_start + c0;
-        s_wcnt[2][d] = local_start + c0 + c1;
-        s_wcnt[3][d] = local_start + c0 + c1 + c2;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kIt; ++j) {
-        const uint32_t d = (k[j] >> shift) & mask;
-        const uint32_t pos = s_wcnt[w][d] + rank[j];
-        s_keys[pos] = k[j];
-        s_vals[pos] = v[j];
-    }
-    __syncthreads();
-    const int64_t rem = n - base;
-    const int valid = rem < kT ? (int)rem : kT;  // tail elements sit in the last slots
-    for (int i = tid; i < valid; i += kBlock) {
-        const uint32_t kk = s_keys[i];
-        const uint32_t gpos = s_delta[(kk >> shift) & mask] + (uint32_t)i;
-        keys_out[gpos] = kk;
-        vals_out[gpos] = s_vals[i];
-    }
-}
-
 }  // namespace
 
 GsrRadixPlan gsr_radix_plan(int begin_bit, int end_bit) {
@@ -332,50 +176,6 @@ GsrRadixPlan gsr_radix_plan(int begin_bit, int end_bit) {
         shift += nb;
     }
     return p;
-}
-
-int gsr_onesweep_items(int64_t n) { return n >= (int64_t)4 << 20 ? 16 : 8; }
-
-int64_t gsr_onesweep_status_words(int64_t n) {
-    const int64_t t = (int64_t)kBlock * 8;  // smallest tile
-    return ((n + t - 1) / t + 1) * kRadix;
-}
-
-hipError_t gsr_onesweep_sort(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
-                             uint32_t **vals_alt, int64_t n, int begin_bit, int end_bit,
-                             int hist_state, const GsrOnesweepWs &ws, hipStream_t s) {
-    if (n <= 1) return hipSuccess;
-    const GsrRadixPlan plan = gsr_radix_plan(begin_bit, end_bit);
-    if (hist_state != GSR_HIST_READY) {
-        if (hist_state == GSR_HIST_ZERO_AND_COUNT) {
-            hipError_t e = hipMemsetAsync(ws.ghist, 0,
-                                          sizeof(uint32_t) * kRadix * GSR_RADIX_MAX_PASSES, s);
-            if (e != hipSuccess) return e;
-        }
-        const int64_t blocks = std::min<int64_t>((n + 4095) / 4096, 1024);
-        hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)blocks), dim3(kBlock), 0, s, *keys, n, plan,
-                           ws.ghist);
-    }
-    const int items = gsr_onesweep_items(n);
-    const int64_t nb = (n + (int64_t)kBlock * items - 1) / ((int64_t)kBlock * items);
-    for (int p = 0; p < plan.n; ++p) {
-        const uint32_t epoch = ++*ws.epoch;
-        if (items == 16)
-            hipLaunchKernelGGL(k_rs_onesweep<16>, dim3((unsigned)nb), dim3(kBlock), 0, s, *keys,
-                               *vals, *keys_alt, *vals_alt, n, plan.shift[p], plan.nbits[p],
-                               ws.ghist + p * kRadix, ws.status, ws.ticket, epoch, ws.err);
-        else
-            hipLaunchKernelGGL(k_rs_onesweep<8>, dim3((unsigned)nb), dim3(kBlock), 0, s, *keys,
-                               *vals, *keys_alt, *vals_alt, n, plan.shift[p], plan.nbits[p],
-                               ws.ghist + p * kRadix, ws.status, ws.ticket, epoch, ws.err);
-        uint32_t *t = *keys;
-        *keys = *keys_alt;
-        *keys_alt = t;
-        t = *vals;
-        *vals = *vals_alt;
-        *vals_alt = t;
-    }
-    return hipGetLastError();
 }
 
 hipError_t gsr_launch_digit_scan(uint32_t *hist, int64_t nb, uint32_t *digit_total,

@@ -195,12 +195,10 @@ const char *gsr_stage_name(int i);
  *     contraction and the hardware exp2; changes pixels by float rounding only (tolerance in
  *     tests/gpu_helpers.py).  0 keeps upstream's per-pixel operation order (IEEE, no FMA,
  *     ocml expf).  2 = the fast arithmetic with two pixels per lane in packed float2 math. */
-/*   GSR_OPT_SORT_ONESWEEP (default 0): 1 = one-kernel-per-pass radix sort with decoupled
- *     look-back; 0 = reduce-then-scan (identical results; faster on MI355X at these sizes,
- *     see DESIGN.md). */
 /*   GSR_OPT_TILE_SORT_SHAPE (tuning): tile shape of the pair sort's reduce-then-scan kernels,
  *     0 = 4 waves x 16 keys/lane, 1 = 16x16, 2 = 4x8, 3 = 8x8 (default), 4 = 8x16, 5 = 4x4.
- *     GSR_OPT_DEPTH_SORT_SHAPE: the same for the per-Gaussian depth sort (default 5). */
+ *     (Option ids 3 and 7 -- the onesweep sort and the old depth-sort shape -- are retired:
+ *     the depth sort is the wide-digit sort of depth_sort.hip.) */
 /*   GSR_OPT_FUSED_BINNING (default 1): the pair duplication regenerates each 4096-pair chunk
  *     and performs the tile sort's first radix pass in the same kernel (reduce-then-scan
  *     sort only); 0 = separate duplicate kernel + full sort.  Identical results. */
@@ -220,10 +218,9 @@ const char *gsr_stage_name(int i);
  *     array count and a segment scatter -- instead of regenerating and ranking every pair; the
  *     second pass sorts packed (tile row, Gaussian id) words.  Needs the second-stream ranges,
  *     <= 256 tile columns and rows per strip, P <= 2^(32 - row bits).  Identical results. */
-enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_SORT_ONESWEEP = 3,
+enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2,
        GSR_OPT_TILE_SORT_SHAPE = 4, GSR_OPT_FUSED_BINNING = 5, GSR_OPT_BLEND_WAVE_QUADRANTS = 6,
-       GSR_OPT_DEPTH_SORT_SHAPE = 7, GSR_OPT_SPLIT_COLOR = 8, GSR_OPT_PACKED_PAIRS = 9,
-       GSR_OPT_COLUMN_PAIRS = 10 };
+       GSR_OPT_SPLIT_COLOR = 8, GSR_OPT_PACKED_PAIRS = 9, GSR_OPT_COLUMN_PAIRS = 10 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
 
 #ifdef __cplusplus

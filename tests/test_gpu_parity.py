@@ -226,17 +226,14 @@ def test_headline_config_c3(gpu, c3_oracle, fast):
 
 
 VARIANTS = {  # [(option, alternative value, default), ...]
-    "onesweep": [(_lib.GSR_OPT_SORT_ONESWEEP, 1, 0)],
     "per_pair": [(_lib.GSR_OPT_COLUMN_PAIRS, 0, 1)],
     "unpacked": [(_lib.GSR_OPT_COLUMN_PAIRS, 0, 1), (_lib.GSR_OPT_PACKED_PAIRS, 0, 1)],
     "unfused": [(_lib.GSR_OPT_FUSED_BINNING, 0, 1)],
     "tile_shape0": [(_lib.GSR_OPT_TILE_SORT_SHAPE, 0, 3)],
     "tile_shape5": [(_lib.GSR_OPT_TILE_SORT_SHAPE, 5, 3)],
-    "depth_shape0": [(_lib.GSR_OPT_DEPTH_SORT_SHAPE, 0, 5)],
-    "depth_shape3": [(_lib.GSR_OPT_DEPTH_SORT_SHAPE, 3, 5)],
     "blend_blocks": [(_lib.GSR_OPT_BLEND_WAVE_QUADRANTS, 0, 1)],
     "inline_color": [(_lib.GSR_OPT_SPLIT_COLOR, 0, 1)],
-    "inline_color_onesweep": [(_lib.GSR_OPT_SPLIT_COLOR, 0, 1), (_lib.GSR_OPT_SORT_ONESWEEP, 1, 0)],
+    "inline_color_unfused": [(_lib.GSR_OPT_SPLIT_COLOR, 0, 1), (_lib.GSR_OPT_FUSED_BINNING, 0, 1)],
 }
 
 
@@ -259,9 +256,9 @@ class _options:
 @pytest.mark.parametrize("size", [(1920, 1080), (16, 16), (4200, 64)])
 def test_sort_implementations_agree(gpu, variant, size):
     """The defaults (duplicate fused with the first reduce-then-scan pass, 8x8 sort tiles, one
-    wave per blend quadrant, colour on the second stream) and the alternatives -- onesweep
-    sort, separate duplicate kernel, other sort tile shapes, 4-wave blend blocks, inline
-    colour -- give identical binning and images.  Sizes: 1 tile (tbits = 0) and > 8 bits of
+    wave per blend quadrant, colour on the second stream) and the alternatives -- separate
+    duplicate kernel, other sort tile shapes, 4-wave blend blocks, inline colour -- give
+    identical binning and images.  Sizes: 1 tile (tbits = 0) and > 8 bits of
     tile id in x."""
     w, h = size
     P = 300_000 if w * h > 10_000 else 20_000
@@ -274,7 +271,7 @@ def test_sort_implementations_agree(gpu, variant, size):
         np.testing.assert_array_equal(alt[k], ref[k], err_msg=k)
 
 
-@pytest.mark.parametrize("variant", ["default", "per_pair", "unpacked", "onesweep", "unfused"])
+@pytest.mark.parametrize("variant", ["default", "per_pair", "unpacked", "unfused"])
 def test_long_tile_lists_and_depth_ties(gpu, oracle_mod, variant):
     """Tiles covered by more than 2048 splats (multi-chunk digit runs in the tile sort, long
     blend lists) and half of the Gaussians at one depth (ties: upstream orders them by
@@ -289,6 +286,23 @@ def test_long_tile_lists_and_depth_ties(gpu, oracle_mod, variant):
     with _options(gpu, VARIANTS.get(variant, [])):
         hip = run_hip(s, gpu)
     assert_parity(hip, orc)
+
+
+@pytest.mark.parametrize("spread", [0.0, 2e-4, 0.05, 1.5, 60.0])
+def test_depth_sort_pass_regimes(gpu, oracle_mod, spread):
+    """The depth sort (depth_sort.hip) sorts only the key bits that differ between the kept
+    Gaussians' depths (D = bits of OR ^ AND), in 12-bit passes decided on the device: all
+    depths equal (D = 0), within 2^12 ulps (one pass), within 2^24 (two passes: 2.5..2.55, and
+    2.5..4 across a float exponent) and 2.5..62.5 (three passes, five exponents).  25k Gaussians
+    = 4 sort tiles; off-screen ones are dropped by pass 0 (sentinel keys)."""
+    g = synthetic_gaussians(25000, 3, 31)
+    rng = np.random.default_rng(31)
+    g.xyz[:, 2] = (np.float32(0.5) - rng.random(25000, dtype=np.float32) * np.float32(spread))
+    g.xyz[::5, 2] = g.xyz[1::5, 2]  # ties across tiles
+    s = scene_inputs(g, static_camera(320, 240, (0, 0, 3.0)), 3)
+    orc = run_oracle(oracle_mod, s)
+    assert orc["num_rendered"] > 0
+    assert_parity(run_hip(s, gpu), orc)
 
 
 def test_tile_lists_of_one_depth(gpu, oracle_mod):

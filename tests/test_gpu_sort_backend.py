@@ -39,7 +39,7 @@ def test_sort_backend_contract(gpu, golden):
     np.testing.assert_array_equal(d[out[:, 0]], d[ref[:, 0]])
 
 
-@pytest.mark.parametrize("P", [1, 2, 4095, 4096, 4097, 1_000_000, 6_000_000])
+@pytest.mark.parametrize("P", [1, 2, 4095, 4097, 8191, 8192, 8193, 40_000, 1_000_000, 6_000_000])
 def test_stable_permutation_full_size(gpu, P):
     rng = np.random.default_rng(P)
     xyz = rng.standard_normal((P, 3)).astype(np.float32)
@@ -63,4 +63,23 @@ def test_negative_nan_and_signed_zero_keys(gpu):
     view = np.eye(4, dtype=np.float32)
     idx, depth = depth_argsort(torch.as_tensor(xyz).to(gpu), view, return_depth=True)
     d = depth.cpu().numpy()
+    np.testing.assert_array_equal(idx.cpu().numpy(), np.argsort(d, kind="stable"))
+
+
+@pytest.mark.parametrize("span_bits", [0, 5, 12, 13, 24, 25])
+def test_key_bit_spans(gpu, span_bits):
+    """Depths whose sort keys differ only in their low span_bits bits: the sort runs one, two
+    or three 12-bit passes (decided on the device) and stays the stable argsort."""
+    rng = np.random.default_rng(span_bits)
+    P = 50_000
+    base = np.uint32(0x40400000)  # 3.0
+    off = rng.integers(0, 1 << span_bits, P, dtype=np.uint64).astype(np.uint32) if span_bits else np.zeros(P, np.uint32)
+    off[::3] = off[1::3]  # ties
+    depth = (base + off).view(np.float32)
+    xyz = np.zeros((P, 3), np.float32)
+    xyz[:, 2] = depth
+    view = np.eye(4, dtype=np.float32)
+    idx, d = depth_argsort(torch.as_tensor(xyz).to(gpu), view, return_depth=True)
+    d = d.cpu().numpy()
+    np.testing.assert_array_equal(d.view(np.uint32), depth.view(np.uint32))
     np.testing.assert_array_equal(idx.cpu().numpy(), np.argsort(d, kind="stable"))
