@@ -28,6 +28,9 @@ using namespace gsr;
 
 namespace {
 
+// 8 waves x 8 keys: 2 waves per SIMD, 91 VGPRs -- small enough to share a CU with two blocks
+// of the second stream's colour pass (16 waves x 4 keys is as fast alone but does not fit
+// beside them)
 constexpr int kDW = 8;                  // waves per block
 constexpr int kDThreads = kDW * 64;     // 512
 constexpr int kDIt = 8;                 // keys per lane
@@ -38,7 +41,8 @@ constexpr int kDSub = 6;                // in-LDS sub-pass width
 constexpr int kDSubBins = 1 << kDSub;   // 64
 constexpr int kDPasses = 3;
 static_assert(kDSubBins * kDW == kDThreads, "one thread per (sub-digit, wave) in the rank scan");
-static_assert(kDBins == kDThreads * 8, "eight digit starts per thread in the prologue");
+constexpr int kDPer = kDBins / kDThreads;  // digit starts per thread in the prologue
+static_assert(kDPer == 8, "two 16-B loads of digit totals and of the hist row per thread");
 
 // ctl: [0] kept count, [1] D (key bits to sort), [2..3] unused, then per tile uint4 {OR, AND,
 // kept, 0} of pass 0.
@@ -330,24 +334,21 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
     // s_tab[d] = start of digit d overall + its count in earlier tiles (8 digits per thread:
     // the exclusive scan of the digit totals plus this tile's row of the scanned histogram)
     {
-        const uint32_t d0 = (uint32_t)tid * 8;
-        uint32_t c[8], h[8], sum = 0;
+        const uint32_t d0 = (uint32_t)tid * kDPer;
+        uint4 c0 = make_uint4(0u, 0u, 0u, 0u), c1 = c0, h0 = c0, h1 = c0;
         if (d0 < nbins) {
             const uint4 *t4 = reinterpret_cast<const uint4 *>(digit_total + d0);
-            const uint4 *h4 =
-                reinterpret_cast<const uint4 *>(hist + (int64_t)blockIdx.x * kDBins + d0);
-            const uint4 ta = t4[0], tb = t4[1], ha = h4[0], hb = h4[1];
-            c[0] = ta.x; c[1] = ta.y; c[2] = ta.z; c[3] = ta.w;
-            c[4] = tb.x; c[5] = tb.y; c[6] = tb.z; c[7] = tb.w;
-            h[0] = ha.x; h[1] = ha.y; h[2] = ha.z; h[3] = ha.w;
-            h[4] = hb.x; h[5] = hb.y; h[6] = hb.z; h[7] = hb.w;
-        } else {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) c[i] = h[i] = 0u;
+            const uint4 *h4 = reinterpret_cast<const uint4 *>(hist + (int64_t)blockIdx.x * kDBins + d0);
+            c0 = t4[0];
+            c1 = t4[1];
+            h0 = h4[0];
+            h1 = h4[1];
         }
+        const uint32_t c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const uint32_t h[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        uint32_t sum = 0, tot;
 #pragma unroll
         for (int i = 0; i < 8; ++i) sum += c[i];
-        uint32_t tot;
         uint32_t pre = blockw_exclusive_scan<kDW>(sum, s_tmp, tot);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -355,13 +356,21 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
             pre += c[i];
         }
     }
+#if defined(GSR_DS_PROBE_STOP) && GSR_DS_PROBE_STOP == 1  // tools/micro/ds_probe.hip
+    {
+        uint32_t x = s_tab[tid * kDPer];
+        for (int j = 0; j < kDIt; ++j) x ^= k[j] ^ v[j];
+        if (x == 0x9E3779B9u) perm[0] = x;
+        return;
+    }
+#endif
     // every pass has >= 8 bits: sub-pass A takes 6, sub-pass B the remaining 6 or 2
     int kept = tile_rank_scatter<kDSub>(k, v, keep, shift, s_keys, s_vals, s_wcnt, s_tmp);
-#ifdef GSR_DS_PROBE_NO_SUB_B
-    if (false) {
-#else
-    if (nbits > kDSub) {
+#if defined(GSR_DS_PROBE_STOP) && GSR_DS_PROBE_STOP == 2
+    if (s_keys[tid] == 0x9E3779B9u) perm[0] = s_vals[tid];
+    return;
 #endif
+    if (nbits > kDSub) {
         keep = 0u;
 #pragma unroll
         for (int j = 0; j < kDIt; ++j) {
@@ -385,8 +394,9 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
         if (i == 0 || ((s_keys[i - 1] >> shift) & mask) != d) s_tab[d] -= (uint32_t)i;
     }
     __syncthreads();
-#ifdef GSR_DS_PROBE_NO_STORE  // tools/micro/ds_probe.hip: timing without the output stores
-    if (kept > 0) return;
+#if defined(GSR_DS_PROBE_STOP) && GSR_DS_PROBE_STOP == 3
+    if (s_keys[tid] == 0x9E3779B9u) perm[0] = s_vals[tid] + s_tab[tid];
+    return;
 #endif
     for (int i = tid; i < kept; i += kDThreads) {
         const uint32_t kk = s_keys[i];

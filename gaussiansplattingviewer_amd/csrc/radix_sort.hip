@@ -133,7 +133,9 @@ __global__ __launch_bounds__(kBlock) void k_rs_scan(uint32_t *__restrict__ hist,
     if (threadIdx.x == 0) digit_total[blockIdx.x] = carry;
 }
 
-template <int kW, int kIt, bool kDrop = false>
+// kVals = false: keys only (vals_in / vals_out unused) -- no LDS for values, so more blocks
+// share a CU.
+template <int kW, int kIt, bool kDrop = false, bool kVals = true>
 __global__ __launch_bounds__(kW * 64) void k_rs_downsweep(
     const uint32_t *__restrict__ keys_in, const uint32_t *__restrict__ vals_in,
     uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out, const RsCount cnt,
@@ -141,7 +143,7 @@ __global__ __launch_bounds__(kW * 64) void k_rs_downsweep(
     const uint32_t *__restrict__ digit_total, int64_t nb) {
     constexpr int kT = kW * 64 * kIt;
     __shared__ uint32_t s_keys[kT];
-    __shared__ uint32_t s_vals[kT];
+    __shared__ uint32_t s_vals[kVals ? kT : 1];
     __shared__ RadixTileSmem<kW, kIt> sm;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t n = cnt.d_n ? (int64_t)*cnt.d_n : cnt.n_host;
@@ -153,12 +155,12 @@ __global__ __launch_bounds__(kW * 64) void k_rs_downsweep(
         const int64_t e = base + w * (kT / kW) + j * 64 + lane;
         const bool valid = e < n;
         k[j] = valid ? keys_in[e] : 0xFFFFFFFFu;  // tail -> largest digit, after every real key
-        v[j] = (valid && vals_in) ? vals_in[e] : 0u;  // vals_in == nullptr: keys only
+        v[j] = (kVals && valid) ? vals_in[e] : 0u;
     }
     const int64_t rem = n - base;
     radix_tile_scatter<kW, kIt, kDrop>(k, v, rem < kT ? (int)rem : kT, shift, nbits, hist, nb,
-                                       blockIdx.x, digit_total, keys_out, vals_out, sm, s_keys,
-                                       s_vals);
+                                       blockIdx.x, digit_total, keys_out,
+                                       kVals ? vals_out : nullptr, sm, s_keys, s_vals);
 }
 
 }  // namespace
@@ -210,8 +212,14 @@ static void rts_pass(const uint32_t *k, const uint32_t *v, uint32_t *ko, uint32_
                        k, up_cnt, shift, mask, hist, nb);
     hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, nb, digit_total, cnt,
                        kT);
-    hipLaunchKernelGGL((k_rs_downsweep<kW, kIt, kDrop>), dim3((unsigned)nb), dim3(kW * 64), 0, s,
-                       k, v, ko, vo, cnt, shift, nbits, hist, digit_total, nb);
+    if (v)
+        hipLaunchKernelGGL((k_rs_downsweep<kW, kIt, kDrop, true>), dim3((unsigned)nb),
+                           dim3(kW * 64), 0, s, k, v, ko, vo, cnt, shift, nbits, hist,
+                           digit_total, nb);
+    else
+        hipLaunchKernelGGL((k_rs_downsweep<kW, kIt, kDrop, false>), dim3((unsigned)nb),
+                           dim3(kW * 64), 0, s, k, v, ko, vo, cnt, shift, nbits, hist,
+                           digit_total, nb);
 }
 
 template <int kW, int kIt>

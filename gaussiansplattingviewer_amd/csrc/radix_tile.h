@@ -74,17 +74,21 @@ __device__ __forceinline__ void radix_tile_scatter(
 #pragma unroll
     for (int j = 0; j < kIt; ++j) {
         const uint32_t d = (k[j] >> shift) & mask;
-        uint64_t m = ~0ull;
-        for (int b = 0; b < nbits; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bal = __ballot(bit);
-            m &= bit ? bal : ~bal;
-        }
         const bool keep = !kDrop || k[j] != kDropKey;
-        if (kDrop) m &= __ballot(keep);  // dropped lanes neither count nor take a rank
+        // lanes holding this lane's digit: one ballot per bit, m &= ~(ballot ^ own bit
+        // sign-extended) -- one v_bitop3 per 32-bit half; dropped lanes neither count nor rank
+        const uint64_t m0 = kDrop ? __ballot(keep) : ~0ull;
+        uint32_t mlo = (uint32_t)m0, mhi = (uint32_t)(m0 >> 32);
+        for (int b = 0; b < nbits; ++b) {
+            const uint32_t f = (uint32_t)(((int32_t)(d << (31 - b))) >> 31);
+            const uint64_t bal = __ballot(f != 0u);
+            mlo &= ~((uint32_t)bal ^ f);
+            mhi &= ~((uint32_t)(bal >> 32) ^ f);
+        }
+        const uint64_t m = ((uint64_t)mhi << 32) | mlo;
         const uint32_t prior = sm.wcnt[w][d];
         rank[j] = prior + (uint32_t)__popcll(m & lt_mask);
-        if (keep && lane == 63 - __clzll(m)) sm.wcnt[w][d] = prior + (uint32_t)__popcll(m);
+        if (keep) sm.wcnt[w][d] = prior + (uint32_t)__popcll(m);  // same value from every match
     }
     __syncthreads();
 
