@@ -38,9 +38,10 @@ sys.path.insert(0, REPO)
 from gaussiansplattingviewer_amd import _lib  # noqa: E402
 from gaussiansplattingviewer_amd.camera import cuda_camera_inputs, orbit_eye, static_camera  # noqa: E402
 from gaussiansplattingviewer_amd.gaussian_data import synthetic_gaussians  # noqa: E402
-from gaussiansplattingviewer_amd.rasterizer import rasterize_gaussians_native  # noqa: E402
+from gaussiansplattingviewer_amd.rasterizer import rasterize_gaussians_native, tile_row_pairs  # noqa: E402
 from gaussiansplattingviewer_amd.pipeline import FramePipeline  # noqa: E402
-from gaussiansplattingviewer_amd.strips import StripGather, strip_rows  # noqa: E402
+from gaussiansplattingviewer_amd.strips import (StripBalancer, StripGather, strip_pixel_rows,  # noqa: E402
+                                                strip_rows)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 
@@ -251,19 +252,22 @@ def main():
 
     scene = Scene(args.config, dev)
     W, H = scene.W, scene.H
-    gy = (H + 15) // 16
-    rows = strip_rows(gy, world, rank) if world > 1 else None
+    gy, gx = (H + 15) // 16, (W + 15) // 16
+    rows = None
     if args.sim_strip:
         if world > 1:
             raise SystemExit("--sim-strip is a single-process diagnostic")
         sr, sn = (int(x) for x in args.sim_strip.split("/"))
         rows = strip_rows(gy, sn, sr)
 
-    # N > 1: each rank renders its strip of tile rows; rank 0 gathers the frame (RCCL).  The
-    # gather of frame i runs asynchronously while frame i+1 renders (at most two frames in
-    # flight); the last frame's gather completes inside the timed region.
+    # N > 1: each rank renders its strip of tile rows; rank 0 receives every strip straight
+    # into its frame (RCCL send/recv).  The gather of frame i runs asynchronously while frame
+    # i+1 renders; the last frame's gather completes inside the timed region.  The strip
+    # boundaries follow the blend work: every 8 frames the ranks all-reduce their tile rows'
+    # pair counts and re-split (StripBalancer), identically on every rank.
     gather = (StripGather(H, W, world, rank, device=dev, depth=args.inflight + 1)
               if world > 1 else None)
+    balancer = StripBalancer(gy, gx, world, rank, device=dev) if world > 1 else None
     # frames in flight: frame i renders on stream i % D with context slot i % D, so the next
     # frame's latency-bound preprocess / sort / binning overlap this frame's blend
     pipe = FramePipeline(args.inflight, dev)
@@ -273,11 +277,19 @@ def main():
             if gather is not None:
                 if len(gather.pending) == len(gather.slots) - 1:
                     gather.finish()
-                res = scene.render(i, rows, slot, out_color=gather.next_buffer())
-                gather.submit(res.color)
-            else:
-                res = scene.render(i, rows, slot)
-        return res
+                layout = balancer.layout(i)
+                mine = layout[rank]
+                buf = gather.next_buffer(strip_pixel_rows(mine, H)[1])
+                if mine[1] > mine[0]:
+                    res = scene.render(i, mine, slot, out_color=buf)
+                    K = res.num_rendered
+                    row_pairs = tile_row_pairs(mine[1] - mine[0], local, slot)
+                else:  # more GPUs than tile rows: nothing to render
+                    K, row_pairs = 0, torch.zeros((0,), dtype=torch.int32, device=dev)
+                gather.submit(buf, layout)
+                balancer.observe(i, row_pairs)
+                return K
+            return scene.render(i, rows, slot).num_rendered
 
     def drain():
         while gather is not None and gather.pending:
@@ -316,12 +328,16 @@ def main():
     t0 = time.perf_counter()
     K_total = 0
     for i in range(args.steps):
-        K_total += step(args.warmup + i).num_rendered
+        K_total += step(args.warmup + i)
     drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if balancer is not None:  # the split the timed frames ended with (for the passes below)
+        rows = balancer.current[rank]
+        if rows[1] <= rows[0]:
+            rows = None
     _lib.check(lib.gsr_stage_times(ctx, buf, len(names)), "gsr_stage_times")
     blend_ms_timed = float(buf[names.index("blend")])
 
@@ -409,6 +425,11 @@ def main():
                          "(each event adds a few us); the timed region records the blend's "
                          "two events only",
         "inflight": args.inflight,
+        "strip_layout": (None if balancer is None else
+                         {"tile_rows": [list(t) for t in balancer.current],
+                          "rebalances": len(balancer.history),
+                          "note": "cost-weighted strips (StripBalancer): every 8 frames the "
+                                  "ranks all-reduce their tile rows' pair counts and re-split"}),
         "serial_ms_per_frame": round(serial_ms, 4),
         "serial_note": "one frame in flight at a time (no FramePipeline overlap), this rank",
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 2),

@@ -30,6 +30,7 @@ EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_get_binning", "gsr_mark_visible", "gsr_depth_argsort",
     "gsr_set_timing", "gsr_stage_times", "gsr_stage_name", "gsr_set_option",
     "gsr_ply_probe", "gsr_ply_load", "gsr_disparity_colors", "gsr_pack_image",
+    "gsr_tile_row_pairs",
 )
 
 GSR_PACK_RGBA_F32 = 0
@@ -95,6 +96,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.gsr_get_binning.argtypes = [vp, vp, vp, vp, ctypes.POINTER(i64),
                                     ctypes.POINTER(ctypes.c_int32), vp]
     lib.gsr_mark_visible.argtypes = [vp, vp, i64, vp, vp, vp, vp]
+    lib.gsr_tile_row_pairs.argtypes = [vp, vp, i32, vp]
     lib.gsr_depth_argsort.argtypes = [vp, vp, i64, ctypes.POINTER(ctypes.c_float), vp, vp, vp]
     lib.gsr_set_timing.argtypes = [vp, i32]
     lib.gsr_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_float), i32]
@@ -109,7 +111,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.gsr_pack_image.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                    ctypes.c_int32, vp, vp]
     for name in ("gsr_disparity_colors", "gsr_pack_image", "gsr_create", "gsr_reserve", "gsr_forward", "gsr_get_binning",
-                 "gsr_mark_visible", "gsr_depth_argsort", "gsr_set_timing",
+                 "gsr_mark_visible", "gsr_depth_argsort", "gsr_set_timing", "gsr_tile_row_pairs",
                  "gsr_stage_times", "gsr_set_option", "gsr_ply_probe", "gsr_ply_load"):
         getattr(lib, name).restype = i32
 

@@ -53,7 +53,7 @@ struct gsr_context {
     // per-pair workspace
     DevBuf tile_keys, tile_vals, tile_keys_alt, tile_vals_alt;
     DevBuf ranges_local;
-    DevBuf tile_diff;  // difference-array partials + sum of the second-stream tile ranges
+    DevBuf tile_diff;  // difference-array partials of the second-stream tile ranges
     // pinned: [K from the device scan (debug), unused, K from the pair count, depth key bits D]
     uint64_t *h_total = nullptr;
     unsigned long long *d_hostK = nullptr;  // device view of h_total + 2
@@ -82,7 +82,9 @@ struct gsr_context {
     // GSR_OPT_COLUMN_PAIRS: the first tile-sort pass on (Gaussian, column) segments of the
     // depth-sorted Gaussians instead of per pair (binning.hip k_col_count / k_col_scatter)
     int column_pairs = 1;
-    int color_blocks = 512;    // grid cap of the overlapped colour pass
+    // grid cap of the overlapped colour pass (0 = none: one wave per 64 Gaussians; uncapped
+    // is fastest since the colour streams its rows with few registers, 3,120 vs 3,030 fps)
+    int color_blocks = 0;
     uint32_t blend_xcd_group = 16;  // tuning (env GSR_BLEND_XCD_GROUP)
     int blend_lean = 1;             // tuning (env GSR_BLEND_LEAN=0: record prefetch, 7 waves)
     int aux_low_priority = 1;  // second stream at the lowest priority
@@ -456,7 +458,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     const bool aux_ranges = ctx->split_color && ctx->fused_binning &&
                             ctx->aux_ranges && diff_cells <= kTileDiffMaxCells;
     if (aux_ranges)
-        GSR_TRY(grow(ctx, ctx->tile_diff, (size_t)(kTileDiffBlocks + 1) * diff_cells * 4, s));
+        GSR_TRY(grow(ctx, ctx->tile_diff, (size_t)kTileDiffBlocks * diff_cells * 4, s));
 
     if (P == 0) {  // upstream returns the zero-initialised image without rendering
         GSR_HIP(hipMemsetAsync(out->color, 0, (size_t)3 * rows_out * W * sizeof(float), s),
@@ -542,7 +544,6 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         if (aux_ranges && ctx->aux_ranges == 1) {
             uint32_t *part = static_cast<uint32_t *>(ctx->tile_diff.p);
             GSR_HIP(gsr_launch_tile_ranges_aux(pa.strip_rect, P, gx, rows_tiles, part,
-                                               part + (size_t)kTileDiffBlocks * diff_cells,
                                                static_cast<uint2 *>(ctx->ranges_local.p), ctx->aux),
                     "tile ranges launch");
         }
@@ -550,7 +551,6 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         if (aux_ranges && ctx->aux_ranges != 1) {
             uint32_t *part = static_cast<uint32_t *>(ctx->tile_diff.p);
             GSR_HIP(gsr_launch_tile_ranges_aux(pa.strip_rect, P, gx, rows_tiles, part,
-                                               part + (size_t)kTileDiffBlocks * diff_cells,
                                                static_cast<uint2 *>(ctx->ranges_local.p), ctx->aux),
                     "tile ranges launch");
         }
@@ -805,6 +805,19 @@ int gsr_get_binning(gsr_context *ctx, uint32_t *point_list, uint32_t *point_tile
                 "hipMemcpyAsync(ranges)");
     }
     GSR_HIP(hipStreamSynchronize(s), "gsr_get_binning");
+    return GSR_OK;
+}
+
+int gsr_tile_row_pairs(gsr_context *ctx, uint32_t *row_pairs, int32_t n_rows, void *stream) {
+    if (!ctx) return fail(GSR_E_INVALID, "gsr_tile_row_pairs: NULL context");
+    if (!ctx->have_forward) return fail(GSR_E_STATE, "gsr_tile_row_pairs: no forward yet");
+    const uint32_t rows = ctx->last_re - ctx->last_rb;
+    if (n_rows != (int32_t)rows || (rows > 0 && !row_pairs))
+        return fail(GSR_E_INVALID, "gsr_tile_row_pairs: n_rows must be the strip's " +
+                                       std::to_string(rows) + " tile rows");
+    GSR_HIP(gsr_launch_row_pairs(static_cast<const uint2 *>(ctx->ranges_local.p), ctx->last_gx,
+                                 rows, row_pairs, static_cast<hipStream_t>(stream)),
+            "row pairs launch");
     return GSR_OK;
 }
 

@@ -541,6 +541,20 @@ __global__ __launch_bounds__(kBlock) void k_ranges(const uint32_t *__restrict__ 
     }
 }
 
+// Pair count of every tile row of the strip: block y sums end - start over its gx tiles.
+__global__ __launch_bounds__(kBlock) void k_row_pairs(const uint2 *__restrict__ ranges,
+                                                      uint32_t gx, uint32_t *__restrict__ out) {
+    __shared__ uint32_t s_tmp[4];
+    uint32_t v = 0;
+    for (uint32_t x = threadIdx.x; x < gx; x += kBlock) {
+        const uint2 r = ranges[(size_t)blockIdx.x * gx + x];
+        v += r.y - r.x;
+    }
+    uint32_t total;
+    block256_exclusive_scan(v, s_tmp, total);
+    if (threadIdx.x == 0) out[blockIdx.x] = total;
+}
+
 // Packed pair list -> Gaussian ids (gsr_get_binning).
 __global__ __launch_bounds__(kBlock) void k_unpack_ids(const uint32_t *__restrict__ packed,
                                                        int64_t K, uint32_t mask,
@@ -634,22 +648,29 @@ namespace {
 // The sorted pair list holds each tile's pairs contiguously in tile order, so ranges[t] =
 // [start_t, start_t + count_t) with start_t the exclusive scan of the per-tile pair counts --
 // which depend only on the Gaussians' tile rects, not on any sort.  They are computed on the
-// second stream while the main stream sorts: the rect of every Gaussian with pairs adds the
-// four corners of a 2D difference array (LDS atomics, per block), the blocks' arrays are summed,
-// and one block turns the sum into counts (row then column prefix sums) and ranges (an
-// exclusive scan in tile order).  Tiles without pairs get (0, 0), as upstream's memset leaves
-// them.  Replaces k_ranges, a pass over the K sorted keys on the main stream.
+// second stream while the main stream sorts, in two kernels:
+//   k_tile_diff     -- per block of Gaussians, in LDS: for every tile row y of a rect, a 1D
+//                      difference array over the columns (+1 at x0, -1 at x1), and one over the
+//                      rows of the rect widths (+w at y0, -w at y1); the block's arrays go to
+//                      `partial` (kTileDiffBlocks of them);
+//   k_tile_finalize -- one block per tile row: sums the partials of its row, prefix over x =
+//                      the row's per-tile counts; the row's first offset = the sum of the pair
+//                      counts of the rows above (prefix of the row-width differences, then a
+//                      prefix of those row totals); then an exclusive scan along the row.
+// Tiles without pairs get (0, 0), as upstream's memset leaves them.  Replaces k_ranges, a pass
+// over the K sorted keys on the main stream (the packed pair list has no tile keys to scan).
 constexpr int kDiffThreads = 1024;
 
 __global__ __launch_bounds__(kDiffThreads) void k_tile_diff(const uint2 *__restrict__ strip_rect,
                                                             int64_t P, uint32_t gx, uint32_t rows,
                                                             uint32_t *__restrict__ partial) {
     extern __shared__ uint32_t s_diff[];
-    const uint32_t w1 = gx + 1, cells = w1 * (rows + 1);
+    const uint32_t w1 = gx + 1, cells = gsr_tile_diff_cells(gx, rows);
+    uint32_t *s_rows = s_diff + w1 * rows;  // rows + 1 row-width differences
     for (uint32_t c = threadIdx.x; c < cells; c += kDiffThreads) s_diff[c] = 0u;
     __syncthreads();
     const int64_t b0 = P * blockIdx.x / gridDim.x, b1 = P * (blockIdx.x + 1) / gridDim.x;
-    // 4 rects per thread and step, their loads issued together (a block covers P / 64)
+    // 4 rects per thread and step, their loads issued together
     constexpr int kU = 4;
     for (int64_t i = b0 + threadIdx.x; i < b1; i += kU * kDiffThreads) {
         uint2 r[kU];
@@ -661,12 +682,14 @@ __global__ __launch_bounds__(kDiffThreads) void k_tile_diff(const uint2 *__restr
 #pragma unroll
         for (int k = 0; k < kU; ++k) {
             if (r[k].x == 0u) continue;  // no pairs in the strip (a rect with pairs has width > 0)
-            const uint32_t x0 = r[k].x & 0xFFFFu, x1 = x0 + (r[k].x >> 16);
+            const uint32_t x0 = r[k].x & 0xFFFFu, w = r[k].x >> 16;
             const uint32_t y0 = r[k].y & 0xFFFFu, y1 = y0 + (r[k].y >> 16);
-            atomicAdd(&s_diff[y0 * w1 + x0], 1u);
-            atomicAdd(&s_diff[y0 * w1 + x1], 0xFFFFFFFFu);  // -1 (mod 2^32)
-            atomicAdd(&s_diff[y1 * w1 + x0], 0xFFFFFFFFu);
-            atomicAdd(&s_diff[y1 * w1 + x1], 1u);
+            for (uint32_t y = y0; y < y1; ++y) {
+                atomicAdd(&s_diff[y * w1 + x0], 1u);
+                atomicAdd(&s_diff[y * w1 + x0 + w], 0xFFFFFFFFu);  // -1 (mod 2^32)
+            }
+            atomicAdd(&s_rows[y0], w);
+            atomicAdd(&s_rows[y1], 0u - w);
         }
     }
     __syncthreads();
@@ -674,64 +697,64 @@ __global__ __launch_bounds__(kDiffThreads) void k_tile_diff(const uint2 *__restr
     for (uint32_t c = threadIdx.x; c < cells; c += kDiffThreads) dst[c] = s_diff[c];
 }
 
-__global__ __launch_bounds__(kBlock) void k_tile_diff_reduce(const uint32_t *__restrict__ partial,
-                                                             int nparts, uint32_t cells,
-                                                             uint32_t *__restrict__ diff) {
-    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
-    if (c >= cells) return;
-    uint32_t v = 0;
+// Inclusive scan over the block (kW waves); s_tmp: kW words.  Returns the prefix, total out.
+template <int kW>
+__device__ __forceinline__ uint32_t blockw_inclusive_scan(uint32_t v, uint32_t *s_tmp,
+                                                          uint32_t &total) {
+    return blockw_exclusive_scan<kW>(v, s_tmp, total) + v;
+}
+
+constexpr int kFinThreads = 256;
+__global__ __launch_bounds__(kFinThreads) void k_tile_finalize(const uint32_t *__restrict__ partial,
+                                                               int nparts, uint32_t gx,
+                                                               uint32_t rows,
+                                                               uint2 *__restrict__ ranges) {
+    constexpr int kW = kFinThreads / 64;
+    __shared__ uint32_t s_tmp[kW];
+    const uint32_t y = blockIdx.x, w1 = gx + 1, cells = gsr_tile_diff_cells(gx, rows);
+    const int tid = threadIdx.x;
+    // offset of this row: sum over rows y' < y of rowtotal[y'] = prefix of the width differences
+    uint32_t before = 0;
+    {
+        uint32_t carry_rd = 0, carry_tot = 0;
+        for (uint32_t y0 = 0; y0 < y; y0 += kFinThreads) {
+            const uint32_t yy = y0 + tid;
+            uint32_t rd = 0;
+            if (yy < y)
 #pragma unroll 8
-    for (int b = 0; b < nparts; ++b) v += partial[(int64_t)b * cells + c];
-    diff[c] = v;
-}
-
-__device__ __forceinline__ void wave_prefix_line(uint32_t *s, uint32_t n, uint32_t stride,
-                                                 int lane) {
-    uint32_t carry = 0;
-    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-        const uint32_t i = i0 + lane;
-        const uint32_t v = i < n ? s[i * stride] : 0u;
-        const uint32_t inc = wave_inclusive_scan(v) + carry;
-        if (i < n) s[i * stride] = inc;
-        carry = __shfl(inc, 63);
+                for (int b = 0; b < nparts; ++b) rd += partial[(int64_t)b * cells + w1 * rows + yy];
+            uint32_t t1, t2;
+            const uint32_t rowtotal = blockw_inclusive_scan<kW>(rd, s_tmp, t1) + carry_rd;
+            carry_rd += t1;
+            const uint32_t sum = blockw_inclusive_scan<kW>(yy < y ? rowtotal : 0u, s_tmp, t2);
+            (void)sum;
+            carry_tot += t2;
+        }
+        before = carry_tot;
     }
-}
-
-__global__ __launch_bounds__(kDiffThreads) void k_tile_ranges_from_diff(
-    const uint32_t *__restrict__ diff, uint32_t gx, uint32_t rows, uint2 *__restrict__ ranges) {
-    extern __shared__ uint32_t s_cnt[];
-    __shared__ uint32_t s_tmp[2 * (kDiffThreads / 64) + 1];
-    const uint32_t w1 = gx + 1, cells = w1 * (rows + 1);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int kWaves = kDiffThreads / 64;
-    for (uint32_t c = threadIdx.x; c < cells; c += kDiffThreads) s_cnt[c] = diff[c];
-    __syncthreads();
-    for (uint32_t y = wave; y < rows; y += kWaves) wave_prefix_line(s_cnt + y * w1, gx, 1, lane);
-    __syncthreads();
-    for (uint32_t x = wave; x < gx; x += kWaves) wave_prefix_line(s_cnt + x, rows, w1, lane);
-    __syncthreads();
-    // s_cnt[y * w1 + x] = pairs of tile (x, y); exclusive scan in tile order t = y * gx + x
-    const uint32_t T = gx * rows;
-    const uint32_t per = (T + kDiffThreads - 1) / kDiffThreads;
-    const uint32_t t0 = min(T, threadIdx.x * per), t1 = min(T, t0 + per);
-    uint32_t sum = 0;
-    for (uint32_t t = t0; t < t1; ++t) sum += s_cnt[(t / gx) * w1 + t % gx];
-    uint32_t total;
-    uint32_t start = blockw_exclusive_scan<kWaves>(sum, s_tmp, total);
-    for (uint32_t t = t0; t < t1; ++t) {
-        const uint32_t n = s_cnt[(t / gx) * w1 + t % gx];
-        ranges[t] = n ? make_uint2(start, start + n) : make_uint2(0u, 0u);
-        start += n;
+    // this row's counts: prefix over x of the summed column differences, then an exclusive
+    // scan along the row
+    uint32_t carry_d = 0, start = before;
+    for (uint32_t x0 = 0; x0 < gx; x0 += kFinThreads) {
+        const uint32_t x = x0 + tid;
+        uint32_t d = 0;
+        if (x < gx)
+#pragma unroll 8
+            for (int b = 0; b < nparts; ++b) d += partial[(int64_t)b * cells + y * w1 + x];
+        uint32_t t1, t2;
+        const uint32_t cnt = blockw_inclusive_scan<kW>(d, s_tmp, t1) + carry_d;
+        carry_d += t1;
+        const uint32_t ex = blockw_exclusive_scan<kW>(x < gx ? cnt : 0u, s_tmp, t2) + start;
+        start += t2;
+        if (x < gx) ranges[y * gx + x] = cnt ? make_uint2(ex, ex + cnt) : make_uint2(0u, 0u);
     }
 }
 
 }  // namespace
 
-uint32_t gsr_tile_diff_cells(uint32_t gx, uint32_t rows) { return (gx + 1) * (rows + 1); }
-
 hipError_t gsr_launch_tile_ranges_aux(const uint2 *strip_rect, int64_t P, uint32_t gx,
-                                      uint32_t rows, uint32_t *partial, uint32_t *diff,
-                                      uint2 *ranges, hipStream_t s) {
+                                      uint32_t rows, uint32_t *partial, uint2 *ranges,
+                                      hipStream_t s) {
     const uint32_t cells = gsr_tile_diff_cells(gx, rows);
     const size_t lds = (size_t)cells * 4;
     if (cells > kTileDiffMaxCells) return hipErrorInvalidValue;
@@ -745,19 +768,13 @@ hipError_t gsr_launch_tile_ranges_aux(const uint2 *strip_rect, int64_t P, uint32
     if (!bit || !(attr_done.load(std::memory_order_acquire) & bit)) {
         e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_tile_diff),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kTileDiffMaxCells * 4);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_tile_ranges_from_diff),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    kTileDiffMaxCells * 4);
         if (e != hipSuccess) return e;
         attr_done.fetch_or(bit, std::memory_order_release);
     }
     hipLaunchKernelGGL(k_tile_diff, dim3(kTileDiffBlocks), dim3(kDiffThreads), lds, s, strip_rect,
                        P, gx, rows, partial);
-    hipLaunchKernelGGL(k_tile_diff_reduce, dim3((cells + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                       partial, kTileDiffBlocks, cells, diff);
-    hipLaunchKernelGGL(k_tile_ranges_from_diff, dim3(1), dim3(kDiffThreads), lds, s, diff, gx,
-                       rows, ranges);
+    hipLaunchKernelGGL(k_tile_finalize, dim3(rows), dim3(kFinThreads), 0, s, partial,
+                       kTileDiffBlocks, gx, rows, ranges);
     return hipGetLastError();
 }
 
@@ -774,6 +791,13 @@ hipError_t gsr_launch_globalize_tiles(const uint32_t *local, int64_t K, uint32_t
     if (K == 0) return hipSuccess;
     hipLaunchKernelGGL(k_globalize, dim3((unsigned)((K + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        s, local, K, offset, global);
+    return hipGetLastError();
+}
+
+hipError_t gsr_launch_row_pairs(const uint2 *ranges, uint32_t gx, uint32_t rows, uint32_t *out,
+                                hipStream_t s) {
+    if (rows == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_row_pairs, dim3(rows), dim3(kBlock), 0, s, ranges, gx, out);
     return hipGetLastError();
 }
 

@@ -329,15 +329,21 @@ hipError_t gsr_launch_fill_tiles(const uint2 *ranges, uint32_t n_tiles, uint32_t
 hipError_t gsr_launch_ranges(const uint32_t *tile_keys, int64_t K, uint32_t *ranges,
                              hipStream_t s);
 // Tile ranges from the Gaussians' strip tile rects alone (no sorted keys): per-tile pair
-// counts via a 2D difference array, then an exclusive scan; runs on the second stream.
-// partial: kTileDiffBlocks * cells words, diff: cells words, cells = gsr_tile_diff_cells(...)
-// <= kTileDiffMaxCells (the difference array lives in LDS).
+// counts via per-row difference arrays, then an exclusive scan; runs on the second stream.
+// partial: kTileDiffBlocks * cells words, cells = gsr_tile_diff_cells(...) <= kTileDiffMaxCells
+// (the difference arrays live in LDS).
 constexpr int kTileDiffBlocks = 64;
 constexpr uint32_t kTileDiffMaxCells = 38912;  // 152 KiB of LDS
-uint32_t gsr_tile_diff_cells(uint32_t gx, uint32_t rows);
+// (gx + 1) column-difference cells per tile row, then rows + 1 row-width differences
+__host__ __device__ inline uint32_t gsr_tile_diff_cells(uint32_t gx, uint32_t rows) {
+    return (gx + 1) * rows + rows + 1;
+}
 hipError_t gsr_launch_tile_ranges_aux(const uint2 *strip_rect, int64_t P, uint32_t gx,
-                                      uint32_t rows, uint32_t *partial, uint32_t *diff,
-                                      uint2 *ranges, hipStream_t s);
+                                      uint32_t rows, uint32_t *partial, uint2 *ranges,
+                                      hipStream_t s);
+// Pair count per tile row of a strip's ranges (gsr_tile_row_pairs).
+hipError_t gsr_launch_row_pairs(const uint2 *ranges, uint32_t gx, uint32_t rows, uint32_t *out,
+                                hipStream_t s);
 hipError_t gsr_launch_globalize_tiles(const uint32_t *local, int64_t K, uint32_t offset,
                                       uint32_t *global, hipStream_t s);
 

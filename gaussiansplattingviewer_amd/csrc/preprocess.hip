@@ -112,6 +112,56 @@ __device__ __forceinline__ float3 eval_sh(float3 pos, const float *campos, const
     return make_float3(fmaxf(r0, 0.0f), fmaxf(r1, 0.0f), fmaxf(r2, 0.0f));
 }
 
+// Degree-3 colour with the coefficients streamed from a 12-float4 row (k_color's LDS image):
+// exactly eval_sh's operations in eval_sh's order -- per channel, the basis terms in increasing
+// order, subtracted for basis 1 and 3 as upstream writes them -- but each coefficient is
+// consumed as it is read, so the row never sits in 48 registers.
+__device__ __forceinline__ float3 eval_sh3_stream(float3 pos, const float *campos,
+                                                  const float4 *row) {
+    float dx = pos.x - campos[0], dy = pos.y - campos[1], dz = pos.z - campos[2];
+    const float len = sqrtf(dx * dx + dy * dy + dz * dz);
+    dx = dx / len;
+    dy = dy / len;
+    dz = dz / len;
+    const float x = dx, y = dy, z = dz;
+    const float xx = x * x, yy = y * y, zz = z * z;
+    const float xy = x * y, yz = y * z, xz = x * z;
+    const float bs[16] = {kShC0,
+                          kShC1 * y,
+                          kShC1 * z,
+                          kShC1 * x,
+                          kShC2[0] * xy,
+                          kShC2[1] * yz,
+                          kShC2[2] * (2.0f * zz - xx - yy),
+                          kShC2[3] * xz,
+                          kShC2[4] * (xx - yy),
+                          kShC3[0] * y * (3.0f * xx - yy),
+                          kShC3[1] * xy * z,
+                          kShC3[2] * y * (4.0f * zz - xx - yy),
+                          kShC3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy),
+                          kShC3[4] * x * (4.0f * zz - xx - yy),
+                          kShC3[5] * z * (xx - yy),
+                          kShC3[6] * x * (xx - 3.0f * yy)};
+    float r[3];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        const float4 q = row[i];
+        const float v[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = 4 * i + u, b = k / 3, ch = k % 3;
+            if (b == 0)
+                r[ch] = bs[0] * v[u];
+            else if (b == 1 || b == 3)
+                r[ch] = r[ch] - bs[b] * v[u];
+            else
+                r[ch] = r[ch] + bs[b] * v[u];
+        }
+    }
+    return make_float3(fmaxf(r[0] + 0.5f, 0.0f), fmaxf(r[1] + 0.5f, 0.0f),
+                       fmaxf(r[2] + 0.5f, 0.0f));
+}
+
 // Conservative cull data of one splat for the blend: the region where it can reach
 // alpha >= 1/255 is  q(d) = A dx^2 + 2B dx dy + C dy^2 <= 2 L,  L = ln(255 o)  (upstream
 // alpha = min(0.99, o exp(power)), power = -q/2).  Returns {ex, ey, Lm}: Lm >= L widened by an
@@ -317,10 +367,30 @@ __device__ __forceinline__ void color_one(const GsrPreprocessArgs &a, int64_t id
 // degree-3 rows (M = 16, a.sh_vec4) a wave reads its 64 rows -- 12 KiB, contiguous -- with
 // fully coalesced 16-B loads (lane l takes float4 i*64 + l), transposes them through LDS
 // (rows padded to 13 float4 so the per-lane 16-B reads are bank-conflict free) and each lane
-// evaluates its own row; rows of invisible Gaussians are skipped when the whole wave is
-// invisible.  Otherwise -- or when fewer than 16 of the wave's 64 Gaussians need a colour --
-// every lane that needs one reads its own row (color_from_sh).
+// evaluates its own row, consuming the coefficients as it reads them (eval_sh3_stream); rows of
+// invisible Gaussians are skipped when the whole wave is invisible.  When fewer than 16 of the
+// wave's 64 Gaussians need a colour every lane that needs one reads its own row instead.
 constexpr int kShRowPad = 13;  // float4 per LDS row
+// The general case (colors_precomp, unaligned rows, degree < 3): one thread per Gaussian.
+__global__ __launch_bounds__(256) void k_color_generic(const GsrPreprocessArgs a) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx < a.P) color_one(a, idx);
+}
+
+// Writes one colour (and the rgb output) of Gaussian idx.
+__device__ __forceinline__ void store_color(const GsrPreprocessArgs &a, int64_t idx, float3 col) {
+    if (a.rgb) {
+        a.rgb[3 * idx] = col.x;
+        a.rgb[3 * idx + 1] = col.y;
+        a.rgb[3 * idx + 2] = col.z;
+    }
+    float *cc = &a.records[idx].c.x;
+    cc[1] = col.x;
+    cc[2] = col.y;
+    cc[3] = col.z;
+}
+
+// Degree 3, 16-B aligned rows, SH input (the host launches k_color_generic otherwise).
 __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
     __shared__ float4 s_sh[4][64 * kShRowPad];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -336,8 +406,13 @@ __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
         if (vis_mask == 0ull) continue;
         // few colours needed in this wave (a strip of a multi-GPU frame): per-lane row reads
         // move only the needed rows, not the wave's whole 12 KiB
-        if (!a.sh_vec4 || a.colors_precomp || a.D != 3 || __popcll(vis_mask) < 16) {
-            if (vis) color_one(a, idx);
+        if (__popcll(vis_mask) < 16) {
+            if (vis) {
+                const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1],
+                                             a.means3D[3 * idx + 2]);
+                store_color(a, idx, eval_sh3_stream(p, a.campos,
+                                                    reinterpret_cast<const float4 *>(a.shs) + idx * 12));
+            }
             continue;
         }
         const float4 *rows = reinterpret_cast<const float4 *>(a.shs) + base * 12;
@@ -349,27 +424,9 @@ __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
         }
         // one wave: its LDS writes complete before its reads below
         if (vis) {
-            float c[48];
-#pragma unroll
-            for (int i = 0; i < 12; ++i) {
-                const float4 q = s_sh[w][lane * kShRowPad + i];
-                c[4 * i + 0] = q.x;
-                c[4 * i + 1] = q.y;
-                c[4 * i + 2] = q.z;
-                c[4 * i + 3] = q.w;
-            }
             const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1],
                                          a.means3D[3 * idx + 2]);
-            const float3 col = eval_sh(p, a.campos, c, 3);
-            if (a.rgb) {
-                a.rgb[3 * idx] = col.x;
-                a.rgb[3 * idx + 1] = col.y;
-                a.rgb[3 * idx + 2] = col.z;
-            }
-            float *cc = &a.records[idx].c.x;
-            cc[1] = col.x;
-            cc[2] = col.y;
-            cc[3] = col.z;
+            store_color(a, idx, eval_sh3_stream(p, a.campos, &s_sh[w][lane * kShRowPad]));
         }
         // the next iteration's LDS writes follow this wave's reads in order
     }
@@ -464,6 +521,10 @@ hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, bool with_color, hi
 hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, hipStream_t s) {
     if (a.P == 0) return hipSuccess;
     const unsigned g0 = grid_for(a.P);  // 4 waves of 64 Gaussians per block
+    if (!a.sh_vec4 || a.colors_precomp || a.D != 3) {
+        hipLaunchKernelGGL(k_color_generic, dim3(g0), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     const unsigned g = max_blocks > 0 && (unsigned)max_blocks < g0 ? max_blocks : g0;
     hipLaunchKernelGGL(k_color, dim3(g), dim3(256), 0, s, a);
     return hipGetLastError();

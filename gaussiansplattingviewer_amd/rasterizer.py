@@ -255,3 +255,19 @@ def binning_state(device_index: int = 0, slot: int = 0):
     _lib.check(lib.gsr_get_binning(ctx, _lib.ptr(pl), _lib.ptr(pt), _lib.ptr(rg), None, None,
                                    stream), "gsr_get_binning")
     return pl, pt, rg
+
+
+def tile_row_pairs(n_rows: int, device_index: int = 0, slot: int = 0, out=None,
+                   stream=None) -> torch.Tensor:
+    """Pair count of every tile row of the last forward's strip on a device's context slot
+    (gsr_tile_row_pairs), as a device int32 tensor of n_rows uint32 values, written on `stream`
+    (default: the current stream) without synchronising.  strips.StripBalancer weights the
+    next frame's strip boundaries by these counts."""
+    lib = _lib.load_library()
+    ctx = _lib.context(device_index, slot)
+    if out is None:
+        out = torch.empty((n_rows,), dtype=torch.int32, device=torch.device("cuda", device_index))
+    s = stream if stream is not None else torch.cuda.current_stream(device_index)
+    _lib.check(lib.gsr_tile_row_pairs(ctx, _lib.ptr(out), int(n_rows),
+                                      ctypes.c_void_p(s.cuda_stream)), "gsr_tile_row_pairs")
+    return out

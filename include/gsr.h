@@ -122,6 +122,13 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
 int gsr_get_binning(gsr_context *ctx, uint32_t *point_list, uint32_t *point_tiles,
                     uint32_t *ranges, int64_t *num_rendered, int32_t *num_tiles, void *stream);
 
+/* Per tile row of the last gsr_forward's strip, its (Gaussian, tile) pair count:
+ * row_pairs[r] for r < n_rows = tile_row_end - tile_row_begin (DEVICE buffer, written on
+ * `stream`, no synchronisation).  The multi-GPU strip split (strips.StripBalancer) weights its
+ * next boundaries by these counts.  No reference counterpart: the reference renders each frame
+ * on one device (renderer_cuda.py:205-224). */
+int gsr_tile_row_pairs(gsr_context *ctx, uint32_t *row_pairs, int32_t n_rows, void *stream);
+
 /* GaussianRasterizer.markVisible: visible[i] = view-space z > 0.2. */
 int gsr_mark_visible(gsr_context *ctx, const float *means3D, int64_t P, const float *viewmatrix,
                      const float *projmatrix, uint8_t *visible, void *stream);

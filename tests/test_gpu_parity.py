@@ -198,6 +198,43 @@ def test_strips_equal_full_frame_rows(gpu, world):
     assert K_sum == full["num_rendered"]
 
 
+def test_cost_weighted_strips_on_a_crowded_scene(gpu):
+    """Strips split by the blend work of a scene crowded into the upper left of the image
+    (the pair counts per tile row from gsr_tile_row_pairs of the full frame, as
+    strips.StripBalancer uses them): the per-row counts equal the full frame's ranges, the
+    weighted split differs from the equal one, and every strip is bit-identical to the rows of
+    the full frame."""
+    import torch
+    from gaussiansplattingviewer_amd.rasterizer import tile_row_pairs
+    from gaussiansplattingviewer_amd.strips import (balanced_layout, strip_layout,
+                                                    strip_pixel_rows)
+    W, H, world = 1280, 720, 8
+    g = synthetic_gaussians(200_000, 3, 25)
+    rng = np.random.default_rng(25)
+    crowd = rng.random(len(g.xyz)) < 0.8  # 80% of the splats in one corner
+    g.xyz[crowd, 0] = g.xyz[crowd, 0] * np.float32(0.3) - np.float32(0.6)
+    g.xyz[crowd, 1] = g.xyz[crowd, 1] * np.float32(0.3) + np.float32(0.5)
+    s = scene_inputs(g, static_camera(W, H), 3)
+    full = run_hip(s, gpu)
+    gy, gx = (H + 15) // 16, (W + 15) // 16
+    rp = tile_row_pairs(gy).cpu().numpy().view(np.uint32).astype(np.int64)
+    rg = full["ranges"].astype(np.int64).reshape(gy, gx, 2)
+    np.testing.assert_array_equal(rp, (rg[..., 1] - rg[..., 0]).sum(axis=1))
+    layout = balanced_layout(rp + 64 * gx, world)
+    assert layout != strip_layout(gy, world)
+    loads = [int(rp[b:e].sum()) for b, e in layout]
+    equal = [int(rp[b:e].sum()) for b, e in strip_layout(gy, world)]
+    assert max(loads) < max(equal)
+    for rows in layout:
+        part = run_hip(s, gpu, tile_rows=rows, binning=False)
+        y0, n = strip_pixel_rows(rows, H)
+        np.testing.assert_array_equal(part["color"].view(np.uint32),
+                                      full["color"][:, y0:y0 + n].view(np.uint32))
+        np.testing.assert_array_equal(part["n_contrib"], full["n_contrib"][y0:y0 + n])
+        sub = tile_row_pairs(rows[1] - rows[0]).cpu().numpy().view(np.uint32)
+        np.testing.assert_array_equal(sub, rp[rows[0]:rows[1]])
+
+
 def test_debug_mode_and_repeatability(gpu):
     s = scene_inputs(synthetic_gaussians(50_000, 3, 19), static_camera(960, 540), 3)
     a = run_hip(s, gpu, debug=True)

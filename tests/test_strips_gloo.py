@@ -60,28 +60,42 @@ def test_gather_strips_reassembles_frame(tmp_path, oracle_mod, world, H, W):
     np.testing.assert_array_equal(out.view(np.uint32), frame.view(np.uint32))
 
 
+def _layouts(H, world, n):
+    """A different split for every frame: the equal one, then boundaries moved around
+    (including empty strips when rows run out)."""
+    from gaussiansplattingviewer_amd.strips import balanced_layout, strip_layout
+    gy = (H + 15) // 16
+    rng = np.random.default_rng(world * 100 + H)
+    out = [strip_layout(gy, world)]
+    for _ in range(n - 1):
+        out.append(balanced_layout(rng.integers(0, 1000, gy), world))
+    return out
+
+
 def _stream_worker(rank, world, port, H, W, result_path, in_place=False):
     from gaussiansplattingviewer_amd.strips import StripGather
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        gy = (H + 15) // 16
-        y0, rows = strip_pixel_rows(strip_rows(gy, world, rank), H)
         frames = [torch.arange(3 * H * W, dtype=torch.float32).reshape(3, H, W) * (k + 1)
                   for k in range(5)]
+        layouts = _layouts(H, world, len(frames))
         sg = StripGather(H, W, world, rank, depth=2)
         got = []
         for k, f in enumerate(frames):  # pipelined: frame k's gather overlaps frame k+1
+            y0, rows = strip_pixel_rows(layouts[k][rank], H)
             if in_place:  # render straight into the send buffer (the bench's path)
-                buf = sg.next_buffer()
+                buf = sg.next_buffer(rows)
                 buf.copy_(f[:, y0:y0 + rows])
-                sg.submit(buf)
+                sg.submit(buf, layouts[k])
             else:
-                sg.submit(f[:, y0:y0 + rows].clone())
+                sg.submit(f[:, y0:y0 + rows].clone(), layouts[k])
             if k >= 1:
-                got.append(sg.finish())
-        got.append(sg.finish())
+                r = sg.finish()
+                got.append(None if r is None else r.clone())
+        r = sg.finish()
+        got.append(None if r is None else r.clone())
         if rank == 0:
             np.save(result_path, torch.stack(got).numpy())
         else:
@@ -91,10 +105,12 @@ def _stream_worker(rank, world, port, H, W, result_path, in_place=False):
 
 
 @pytest.mark.parametrize("world,H,W,in_place", [(2, 100, 48, False), (3, 100, 48, False),
-                                                (3, 100, 48, True), (2, 36, 40, True)])
+                                                (3, 100, 48, True), (2, 36, 40, True),
+                                                (4, 40, 24, True)])
 def test_strip_gather_pipelined_stream(tmp_path, world, H, W, in_place):
-    """StripGather (the bench's pipelined gather): 5 frames, two in flight, reassembled in
-    order and bit-exact on rank 0; strips copied in or rendered into the send buffers."""
+    """StripGather (the bench's pipelined gather): 5 frames, two in flight, each with its own
+    strip boundaries, received straight into rank 0's frame, in order and bit-exact; strips
+    copied in or rendered into the send buffers."""
     rp = tmp_path / "out.npy"
     mp.start_processes(_stream_worker, args=(world, _free_port(), H, W, str(rp), in_place),
                        nprocs=world,
@@ -103,3 +119,65 @@ def test_strip_gather_pipelined_stream(tmp_path, world, H, W, in_place):
     want = np.stack([np.arange(3 * H * W, dtype=np.float32).reshape(3, H, W) * (k + 1)
                      for k in range(5)])
     np.testing.assert_array_equal(out, want)
+
+
+def _balancer_worker(rank, world, port, gy, gx, result_path):
+    from gaussiansplattingviewer_amd.strips import StripBalancer
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # the scene's pair counts per tile row: crowded at the top of the image
+        costs = (np.arange(gy)[::-1] ** 2 * 50).astype(np.int32)
+        bal = StripBalancer(gy, gx, world, rank, every=4, lag=2, tile_cost=8)
+        seen = []
+        for f in range(13):
+            lay = bal.layout(f)
+            seen.append([list(t) for t in lay])
+            b, e = lay[rank]
+            bal.observe(f, torch.from_numpy(costs[b:e].copy()))
+        np.save(result_path + f".{rank}.npy", np.array(seen, dtype=np.int64))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,gy", [(2, 68), (3, 20), (4, 9)])
+def test_strip_balancer_consistent_and_weighted(tmp_path, world, gy):
+    """StripBalancer: every rank switches to the same cost-weighted split on the same frame
+    (observe every 4 frames, applied 2 frames later), and that split is balanced_layout of the
+    all-reduced row costs plus the per-tile constant."""
+    from gaussiansplattingviewer_amd.strips import balanced_layout, strip_layout
+    gx = 30
+    rp = str(tmp_path / "lay")
+    mp.start_processes(_balancer_worker, args=(world, _free_port(), gy, gx, rp), nprocs=world,
+                       join=True, start_method="spawn")
+    seen = [np.load(rp + f".{r}.npy") for r in range(world)]
+    for r in range(1, world):
+        np.testing.assert_array_equal(seen[r], seen[0])
+    costs = np.arange(gy)[::-1] ** 2 * 50
+    want = np.array(balanced_layout(costs + 8 * gx, world))
+    np.testing.assert_array_equal(seen[0][0], np.array(strip_layout(gy, world)))
+    np.testing.assert_array_equal(seen[0][1], np.array(strip_layout(gy, world)))
+    np.testing.assert_array_equal(seen[0][2], want)  # observed at 0, applied at 2
+    np.testing.assert_array_equal(seen[0][-1], want)
+    assert not np.array_equal(want, np.array(strip_layout(gy, world)))
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_balanced_layout_properties(seed):
+    """balanced_layout: contiguous cover of all rows, >= 1 row per strip when rows allow,
+    and no strip heavier than its ideal share plus the heaviest single row."""
+    from gaussiansplattingviewer_amd.strips import balanced_layout
+    rng = np.random.default_rng(seed)
+    gy = int(rng.integers(1, 140))
+    world = int(rng.integers(1, 9))
+    c = rng.integers(0, 5000, gy) * (rng.random(gy) < 0.6)
+    lay = balanced_layout(c, world)
+    assert len(lay) == world and lay[0][0] == 0 and lay[-1][1] == gy
+    for (b0, e0), (b1, e1) in zip(lay, lay[1:]):
+        assert e0 == b1 and b0 <= e0
+    if gy >= world:
+        assert all(e > b for b, e in lay)
+    loads = [int(c[b:e].sum()) for b, e in lay]
+    if c.sum() > 0 and gy >= world:
+        assert max(loads) <= c.sum() / world + c.max() * 2
