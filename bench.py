@@ -69,9 +69,7 @@ def parse():
                          "gather) to estimate one rank's share of an N-GPU frame")
     ap.add_argument("--inline-color", action="store_true",
                     help="GSR_OPT_SPLIT_COLOR=0: colour inside the preprocess kernel (tuning)")
-    ap.add_argument("--blend-blocks", action="store_true",
-                    help="GSR_OPT_BLEND_WAVE_QUADRANTS=0: 4-wave block per tile (tuning)")
-    ap.add_argument("--blend", default="fast", choices=["exact", "fast", "packed"],
+    ap.add_argument("--blend", default="fast", choices=["exact", "fast"],
                     help="blend arithmetic: GSR_OPT_BLEND_FAST (default) or upstream's exact "
                          "operation order")
     ap.add_argument("--inflight", type=int, default=2,
@@ -300,11 +298,9 @@ def main():
     ctx = ctxs[0]  # stage timing is read from slot 0 (every D-th frame)
     for c in ctxs:
         opt = lambda o, v: _lib.check(lib.gsr_set_option(c, o, v), "gsr_set_option")  # noqa: E731
-        opt(_lib.GSR_OPT_BLEND_FAST, {"exact": 0, "fast": 1, "packed": 2}[args.blend])
+        opt(_lib.GSR_OPT_BLEND_FAST, {"exact": 0, "fast": 1}[args.blend])
         if args.sort_shape is not None:
             opt(_lib.GSR_OPT_TILE_SORT_SHAPE, args.sort_shape)
-        if args.blend_blocks:
-            opt(_lib.GSR_OPT_BLEND_WAVE_QUADRANTS, 0)
         if args.inline_color:
             opt(_lib.GSR_OPT_SPLIT_COLOR, 0)
         if args.unfused:
@@ -393,7 +389,7 @@ def main():
     dom_ms = stage_ms[dominant]
     ach = alg[dominant] / (dom_ms * 1e-3) / 1e9
     default_opts = not (args.sort_shape is not None or
-                        args.unfused or args.blend_blocks or args.inline_color or
+                        args.unfused or args.inline_color or
                         args.blend != "fast")
     traffic, traffic_src = measured_traffic(dominant, args.config, default_opts)
     fps = args.steps / t_max

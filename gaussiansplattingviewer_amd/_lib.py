@@ -19,7 +19,6 @@ GSR_OPT_BLEND_CULL = 1
 GSR_OPT_BLEND_FAST = 2
 GSR_OPT_TILE_SORT_SHAPE = 4
 GSR_OPT_FUSED_BINNING = 5
-GSR_OPT_BLEND_WAVE_QUADRANTS = 6
 GSR_OPT_SPLIT_COLOR = 8
 GSR_OPT_PACKED_PAIRS = 9
 GSR_OPT_COLUMN_PAIRS = 10

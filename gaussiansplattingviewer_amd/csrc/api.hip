@@ -74,7 +74,6 @@ struct gsr_context {
     // (2; 1 = before it: the colour then overlaps the duplicate stage instead of the depth
     // sort and the frame is ~2% slower; 0 = k_ranges on the main stream).  env GSR_AUX_RANGES
     int aux_ranges = 2;
-    int blend_wave_quadrants = 1;
     // GSR_OPT_PACKED_PAIRS: one 32-bit word per (tile, Gaussian) pair -- the tile-id bits the
     // second tile-sort pass needs above the Gaussian id -- instead of a key and a value array
     // (needs the second-stream ranges; falls back when the bits do not fit)
@@ -86,7 +85,6 @@ struct gsr_context {
     // is fastest since the colour streams its rows with few registers, 3,120 vs 3,030 fps)
     int color_blocks = 0;
     uint32_t blend_xcd_group = 16;  // tuning (env GSR_BLEND_XCD_GROUP)
-    int blend_lean = 1;             // tuning (env GSR_BLEND_LEAN=0: record prefetch, 7 waves)
     int aux_low_priority = 1;  // second stream at the lowest priority
     bool serial_color = false; // tuning (env GSR_SERIAL_COLOR): join right after the fork
     bool late_K = false;       // tuning (env GSR_LATE_K): also sync on the scan's total
@@ -101,7 +99,6 @@ struct gsr_context {
     // before the blend
     hipStream_t aux = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
-    unsigned long long *blend_stamps = nullptr;  // diagnostics, env GSR_DEBUG_BLEND_STAMPS
 };
 
 namespace {
@@ -222,8 +219,6 @@ int gsr_create(gsr_context **out) {
     ctx->aux_low_priority = env_prio ? std::atoi(env_prio) : 1;
     const char *env_cb = std::getenv("GSR_COLOR_BLOCKS");    // tuning: grid cap, 0 = none
     if (env_cb) ctx->color_blocks = std::atoi(env_cb);
-    const char *env_ln = std::getenv("GSR_BLEND_LEAN");
-    if (env_ln) ctx->blend_lean = std::atoi(env_ln);
     const char *env_cp = std::getenv("GSR_COLUMN_PAIRS");
     if (env_cp) ctx->column_pairs = std::atoi(env_cp);
     const char *env_pp = std::getenv("GSR_PACKED_PAIRS");
@@ -251,13 +246,6 @@ int gsr_create(gsr_context **out) {
         (void)hipGetLastError();
         gsr_destroy(ctx);
         return fail(GSR_E_HIP, "gsr_create: stream / event creation failed");
-    }
-    if (std::getenv("GSR_DEBUG_BLEND_STAMPS")) {
-        if (hipMalloc(reinterpret_cast<void **>(&ctx->blend_stamps), 256 * 8 * 8) != hipSuccess ||
-            hipMemset(ctx->blend_stamps, 0, 256 * 8 * 8) != hipSuccess) {
-            (void)hipGetLastError();
-            ctx->blend_stamps = nullptr;
-        }
     }
     *out = ctx;
     return GSR_OK;
@@ -288,18 +276,6 @@ void gsr_destroy(gsr_context *ctx) {
     if (ctx->kcount_ready) (void)hipEventDestroy(ctx->kcount_ready);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->h_total) (void)hipHostFree(ctx->h_total);
-    if (ctx->blend_stamps) {
-        static unsigned long long sh[256 * 8];
-        unsigned long long h[8] = {};
-        (void)hipMemcpy(sh, ctx->blend_stamps, sizeof(sh), hipMemcpyDeviceToHost);
-        for (int i = 0; i < 256 * 8; ++i) h[i % 8] += sh[i];
-        const double waves = h[5] ? (double)h[5] : 1.0;
-        std::fprintf(stderr,
-                     "[gsr blend stamps] per wave: staging+barriers %.0f, lists %.0f, "
-                     "compositing %.0f cycles; %.2f batches, %.1f splats composited\n",
-                     h[0] / waves, h[1] / waves, h[2] / waves, h[3] / waves, h[4] / waves);
-        (void)hipFree(ctx->blend_stamps);
-    }
     delete ctx;
 }
 
@@ -318,12 +294,8 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
         return GSR_OK;
     }
     if (option == GSR_OPT_BLEND_FAST) {
-        if (value < 0 || value > 2) return fail(GSR_E_INVALID, "gsr_set_option: fast 0..2");
+        if (value < 0 || value > 1) return fail(GSR_E_INVALID, "gsr_set_option: fast 0..1");
         ctx->fast = (int)value;
-        return GSR_OK;
-    }
-    if (option == GSR_OPT_BLEND_WAVE_QUADRANTS) {
-        ctx->blend_wave_quadrants = value ? 1 : 0;
         return GSR_OK;
     }
     if (option == GSR_OPT_SPLIT_COLOR) {
@@ -745,11 +717,8 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     ba.n_contrib = out->n_contrib;
     ba.cull = ctx->cull;
     ba.fast = ctx->fast;
-    ba.wave_quadrants = ctx->blend_wave_quadrants;
     ba.xcd_group = ctx->blend_xcd_group;
-    ba.lean = ctx->blend_lean;
     ba.id_mask = id_mask;
-    ba.stamps = ctx->blend_stamps;
     GSR_HIP(gsr_launch_blend(ba, s), "blend launch");
     GSR_TRY(stage_end(6));
 

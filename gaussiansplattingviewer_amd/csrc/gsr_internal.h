@@ -357,13 +357,9 @@ struct GsrBlendArgs {
     const float *bg;
     float *out_color, *final_T;
     uint32_t *n_contrib;
-    int cull;
-    int fast;   // 1: folded-constant FMA arithmetic + raw v_exp_f32; 2: same, packed 2 px/lane
-    int wave_quadrants;  // 1: one independent wave per (tile, quadrant) (k_blend_q)
+    int cull;            // 0: no quadrant cull (identical output, tested)
+    int fast;            // 1: folded-constant FMA arithmetic + raw v_exp_f32; 0: upstream order
     uint32_t xcd_group;  // work items per XCD round-robin group (0: plain block order)
-    int lean;            // fast mode: k_blend_q<true, true> (no record prefetch, 8 waves/SIMD)
     uint32_t id_mask;    // point_list word -> Gaussian id (packed pair lists; else ~0u)
-    // diagnostics (env GSR_DEBUG_BLEND_STAMPS): per-phase s_memtime sums, see blend.hip
-    unsigned long long *stamps;
 };
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s);

@@ -201,17 +201,14 @@ const char *gsr_stage_name(int i);
  *   GSR_OPT_BLEND_FAST (default 1): blend arithmetic with log2(e) folded into the conic, FMA
  *     contraction and the hardware exp2; changes pixels by float rounding only (tolerance in
  *     tests/gpu_helpers.py).  0 keeps upstream's per-pixel operation order (IEEE, no FMA,
- *     ocml expf).  2 = the fast arithmetic with two pixels per lane in packed float2 math. */
+ *     ocml expf). */
 /*   GSR_OPT_TILE_SORT_SHAPE (tuning): tile shape of the pair sort's reduce-then-scan kernels,
  *     0 = 4 waves x 16 keys/lane, 1 = 16x16, 2 = 4x8, 3 = 8x8 (default), 4 = 8x16, 5 = 4x4.
- *     (Option ids 3 and 7 -- the onesweep sort and the old depth-sort shape -- are retired:
- *     the depth sort is the wide-digit sort of depth_sort.hip.) */
+ *     (Option ids 3, 6 and 7 -- the onesweep sort, the 4-wave blend blocks and the old
+ *     depth-sort shape -- are retired.) */
 /*   GSR_OPT_FUSED_BINNING (default 1): the pair duplication regenerates each 4096-pair chunk
  *     and performs the tile sort's first radix pass in the same kernel (reduce-then-scan
  *     sort only); 0 = separate duplicate kernel + full sort.  Identical results. */
-/*   GSR_OPT_BLEND_WAVE_QUADRANTS (default 1): the blend runs one independent wave per
- *     (tile, 8x8 quadrant); 0 = one 4-wave block per tile with shared staging.  Identical
- *     results.  (Ignored by GSR_OPT_BLEND_FAST = 2.) */
 /*   GSR_OPT_SPLIT_COLOR (default 1): SH -> RGB runs as its own kernel on an internal second
  *     stream, overlapped with the depth sort and the binning; 0 = inside the preprocess
  *     kernel.  Identical results. */
@@ -226,7 +223,7 @@ const char *gsr_stage_name(int i);
  *     second pass sorts packed (tile row, Gaussian id) words.  Needs the second-stream ranges,
  *     <= 256 tile columns and rows per strip, P <= 2^(32 - row bits).  Identical results. */
 enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2,
-       GSR_OPT_TILE_SORT_SHAPE = 4, GSR_OPT_FUSED_BINNING = 5, GSR_OPT_BLEND_WAVE_QUADRANTS = 6,
+       GSR_OPT_TILE_SORT_SHAPE = 4, GSR_OPT_FUSED_BINNING = 5,
        GSR_OPT_SPLIT_COLOR = 8, GSR_OPT_PACKED_PAIRS = 9, GSR_OPT_COLUMN_PAIRS = 10 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
 

@@ -122,7 +122,7 @@ def test_empty_and_fully_culled(gpu, oracle_mod):
     assert np.all(hip["color"][1] == np.float32(0.2))
 
 
-@pytest.mark.parametrize("fast", [0, 1, 2])
+@pytest.mark.parametrize("fast", [0, 1])
 @pytest.mark.parametrize("scene", ["dense_720p", "elongated_close"])
 def test_cull_is_exact(gpu, fast, scene):
     """The blend's ellipse-vs-quadrant cull changes nothing: bit-identical image either way,
@@ -150,12 +150,12 @@ def test_cull_is_exact(gpu, fast, scene):
         np.testing.assert_array_equal(on[k].view(np.uint32), off[k].view(np.uint32), err_msg=k)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("name", ["C1_10k_640x480_sh3", "C2_100k_1080p_sh0",
                                   "inside_cloud_20k_1160x522_sh3"])
 def test_blend_mode_parity(gpu, oracle_mod, name, mode):
-    """Every blend arithmetic mode (GSR_OPT_BLEND_FAST: 0 = upstream operation order, 1 = fused,
-    2 = fused + packed two pixels per lane): binning bit-exact, image within the tolerance."""
+    """Both blend arithmetic modes (GSR_OPT_BLEND_FAST: 0 = upstream operation order, 1 = fused):
+    binning bit-exact, image within the tolerance."""
     P, W, H, deg, seed, eye = CASES[name]
     s = scene_inputs(synthetic_gaussians(P, deg, seed), static_camera(W, H, eye), deg)
     _set_option(gpu, _lib.GSR_OPT_BLEND_FAST, mode)
@@ -249,7 +249,7 @@ def c3_oracle(oracle_mod):
     return s, run_oracle(oracle_mod, s)
 
 
-@pytest.mark.parametrize("fast", [0, 1, 2])
+@pytest.mark.parametrize("fast", [0, 1])
 def test_headline_config_c3(gpu, c3_oracle, fast):
     """Config C3 at full size: 1M Gaussians, 1920x1080, SH degree 3, static camera."""
     s, orc = c3_oracle
@@ -268,7 +268,7 @@ VARIANTS = {  # [(option, alternative value, default), ...]
     "unfused": [(_lib.GSR_OPT_FUSED_BINNING, 0, 1)],
     "tile_shape0": [(_lib.GSR_OPT_TILE_SORT_SHAPE, 0, 3)],
     "tile_shape5": [(_lib.GSR_OPT_TILE_SORT_SHAPE, 5, 3)],
-    "blend_blocks": [(_lib.GSR_OPT_BLEND_WAVE_QUADRANTS, 0, 1)],
+    "no_cull": [(_lib.GSR_OPT_BLEND_CULL, 0, 1)],
     "inline_color": [(_lib.GSR_OPT_SPLIT_COLOR, 0, 1)],
     "inline_color_unfused": [(_lib.GSR_OPT_SPLIT_COLOR, 0, 1), (_lib.GSR_OPT_FUSED_BINNING, 0, 1)],
 }
@@ -292,10 +292,10 @@ class _options:
 @pytest.mark.parametrize("variant", list(VARIANTS))
 @pytest.mark.parametrize("size", [(1920, 1080), (16, 16), (4200, 64)])
 def test_sort_implementations_agree(gpu, variant, size):
-    """The defaults (duplicate fused with the first reduce-then-scan pass, 8x8 sort tiles, one
-    wave per blend quadrant, colour on the second stream) and the alternatives -- separate
-    duplicate kernel, other sort tile shapes, 4-wave blend blocks, inline colour -- give
-    identical binning and images.  Sizes: 1 tile (tbits = 0) and > 8 bits of
+    """The defaults (duplicate fused with the first reduce-then-scan pass, 8x8 sort tiles, the
+    blend's quadrant cull, colour on the second stream) and the alternatives -- separate
+    duplicate kernel, other sort tile shapes, no cull, inline colour -- give identical binning
+    and images.  Sizes: 1 tile (tbits = 0) and > 8 bits of
     tile id in x."""
     w, h = size
     P = 300_000 if w * h > 10_000 else 20_000
