@@ -136,7 +136,9 @@ def measured_traffic(stage, config, default_opts):
 # command (tools/pmc_sq.sh + tools/sq_summary.py --json).  achieved = SQ_INSTS_VALU (wave64
 # instructions) x 64 lanes / launch time; peak = 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz =
 # 78.6 T lane-instructions/s (the 157.3 TFLOP/s FP32 vector peak counts an FMA as 2 flops).
-# busy = SQ_ACTIVE_INST_VALU (quad-cycles) x 4 / (1024 SIMDs x kernel cycles).
+# busy = SQ_INSTS_VALU x 2 cycles (a wave64 VALU instruction issues over 2 cycles) / (1024
+# SIMDs x kernel cycles).  SQ_INSTS_VALU is exact: it reads the known instruction count of a
+# calibration kernel (tools/micro/valu_calib.hip, profiles/r02_valu_calibration.md).
 VALU_PROFILE = os.path.join(REPO, "profiles", "r02_c3_blend_sq.json")
 VALU_PEAK_T = 256 * 4 * 32 * 2.4e9 / 1e12
 
@@ -154,8 +156,7 @@ def valu_roofline(stage, launch_ms, config, default_opts):
            "valu_wave_instr_per_launch": int(c["SQ_INSTS_VALU"]),
            "waves_per_launch": int(c["SQ_WAVES"]),
            "source": os.path.relpath(VALU_PROFILE, REPO)}
-    if "SQ_ACTIVE_INST_VALU" in c:
-        out["valu_busy"] = round(c["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / cyc, 4)
+    out["valu_busy"] = round(c["SQ_INSTS_VALU"] * 2 / 1024 / cyc, 4)
     return out
 
 

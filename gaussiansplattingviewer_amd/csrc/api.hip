@@ -81,8 +81,10 @@ struct gsr_context {
     // GSR_OPT_COLUMN_PAIRS: the first tile-sort pass on (Gaussian, column) segments of the
     // depth-sorted Gaussians instead of per pair (binning.hip k_col_count / k_col_scatter)
     int column_pairs = 1;
-    // grid cap of the overlapped colour pass (0 = none: one wave per 64 Gaussians; uncapped
-    // is fastest since the colour streams its rows with few registers, 3,120 vs 3,030 fps)
+    // grid cap of the overlapped colour pass (0 = none: one wave per 64 Gaussians).  Uncapped
+    // gives the best frame rate with two frames in flight (C3: 3,186 fps vs 3,010 at 256
+    // blocks); 256 the best serial frame (0.369 vs 0.386 ms): the colour then takes fewer CUs
+    // from the depth sort it overlaps (env GSR_COLOR_BLOCKS)
     int color_blocks = 0;
     uint32_t blend_xcd_group = 16;  // tuning (env GSR_BLEND_XCD_GROUP)
     int aux_low_priority = 1;  // second stream at the lowest priority

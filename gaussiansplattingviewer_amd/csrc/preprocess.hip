@@ -362,15 +362,6 @@ __device__ __forceinline__ void color_one(const GsrPreprocessArgs &a, int64_t id
     c[3] = col.z;
 }
 
-// Grid-stride over waves of 64 Gaussians; the grid is capped (api.hip) so the colour pass,
-// which runs beside the latency-bound depth sort, leaves CUs free for it.  With 16-B aligned
-// degree-3 rows (M = 16, a.sh_vec4) a wave reads its 64 rows -- 12 KiB, contiguous -- with
-// fully coalesced 16-B loads (lane l takes float4 i*64 + l), transposes them through LDS
-// (rows padded to 13 float4 so the per-lane 16-B reads are bank-conflict free) and each lane
-// evaluates its own row, consuming the coefficients as it reads them (eval_sh3_stream); rows of
-// invisible Gaussians are skipped when the whole wave is invisible.  When fewer than 16 of the
-// wave's 64 Gaussians need a colour every lane that needs one reads its own row instead.
-constexpr int kShRowPad = 13;  // float4 per LDS row
 // The general case (colors_precomp, unaligned rows, degree < 3): one thread per Gaussian.
 __global__ __launch_bounds__(256) void k_color_generic(const GsrPreprocessArgs a) {
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -390,45 +381,28 @@ __device__ __forceinline__ void store_color(const GsrPreprocessArgs &a, int64_t 
     cc[3] = col.z;
 }
 
-// Degree 3, 16-B aligned rows, SH input (the host launches k_color_generic otherwise).
+// Degree 3 with 16-B aligned rows (the host launches k_color_generic otherwise), grid-stride
+// over waves of 64 Gaussians (the grid may be capped so the colour pass, which runs beside the
+// latency-bound depth sort on the second stream, leaves CUs free for it; uncapped by default).
+// Every lane that needs a colour reads its own 192-B row with 12 x 16-B loads -- a wave's 64
+// rows are 12 KiB contiguous, so its 12 load instructions hit the same lines and each line
+// leaves L2 once -- and consumes the coefficients as they arrive (eval_sh3_stream).  An LDS
+// transpose of the wave's rows (coalesced loads, 13 KiB of LDS per wave, 130 VGPRs) was
+// slower: 144 vs 83 us per launch at the same grid cap (C3, interleaved A/B on MI355X).
 __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
-    __shared__ float4 s_sh[4][64 * kShRowPad];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t n_waves = (a.P + 63) / 64;
     const int64_t wave_stride = (int64_t)gridDim.x * 4;
     for (int64_t wv = (int64_t)blockIdx.x * 4 + w; wv < n_waves; wv += wave_stride) {
-        const int64_t base = wv * 64, idx = base + lane;
-        const bool in = idx < a.P;
+        const int64_t idx = wv * 64 + lane;
         // colour needed: Gaussians with pairs in this strip (the blend reads them), or every
         // visible one when the caller asked for the rgb output (upstream semantics)
-        const bool vis = in && (a.rgb ? a.radii[idx] != 0 : a.strip_rect[idx].x != 0u);
-        const uint64_t vis_mask = __ballot(vis);
-        if (vis_mask == 0ull) continue;
-        // few colours needed in this wave (a strip of a multi-GPU frame): per-lane row reads
-        // move only the needed rows, not the wave's whole 12 KiB
-        if (__popcll(vis_mask) < 16) {
-            if (vis) {
-                const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1],
-                                             a.means3D[3 * idx + 2]);
-                store_color(a, idx, eval_sh3_stream(p, a.campos,
-                                                    reinterpret_cast<const float4 *>(a.shs) + idx * 12));
-            }
-            continue;
-        }
-        const float4 *rows = reinterpret_cast<const float4 *>(a.shs) + base * 12;
-        const int64_t n_vec = min<int64_t>(64, a.P - base) * 12;
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-            const int v = i * 64 + lane;  // float4 v of the wave's rows: row v / 12, col v % 12
-            if (v < n_vec) s_sh[w][(v / 12) * kShRowPad + v % 12] = rows[v];
-        }
-        // one wave: its LDS writes complete before its reads below
-        if (vis) {
+        if (idx < a.P && (a.rgb ? a.radii[idx] != 0 : a.strip_rect[idx].x != 0u)) {
             const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1],
                                          a.means3D[3 * idx + 2]);
-            store_color(a, idx, eval_sh3_stream(p, a.campos, &s_sh[w][lane * kShRowPad]));
+            store_color(a, idx, eval_sh3_stream(p, a.campos,
+                                                reinterpret_cast<const float4 *>(a.shs) + idx * 12));
         }
-        // the next iteration's LDS writes follow this wave's reads in order
     }
 }
 

@@ -39,8 +39,9 @@ if "SQ_WAVE_CYCLES" in res and "SQ_ACTIVE_INST_ANY" in res:
           f"resident waves/SIMD {4 * wc / cyc / 1024:.1f}")
 print(f"  VALU pipe busy (2 cyc/instr) {res['SQ_INSTS_VALU'] * 2 / 1024 / cyc:.0%}")
 if "SQ_ACTIVE_INST_VALU" in res:
-    print(f"  SQ_ACTIVE_INST_VALU (quad-cycles x4 / SIMD-cycles) "
-          f"{res['SQ_ACTIVE_INST_VALU'] * 4 / 1024 / cyc:.0%}")
+    # counts instructions, like SQ_INSTS_VALU (tools/micro/valu_calib.hip: both read exactly
+    # the known count of a calibration kernel; profiles/r02_valu_calibration.md)
+    print(f"  SQ_ACTIVE_INST_VALU {res['SQ_ACTIVE_INST_VALU'] / 1e6:.1f} M (= VALU instructions)")
 if out_json:
     json.dump({"kernel": kern, "kernels_matched": sorted(names), "source": d,
                "launches": launches, "per_launch": res}, open(out_json, "w"), indent=1)
