@@ -386,9 +386,80 @@ __global__ __launch_bounds__(kFW * 64) void k_dup_scatter(
 // the fused duplicate; the pair list is identical (each tile's pairs in depth order, then
 // Gaussian index; tiles row-major).
 constexpr int kCG = 256;                // depth-sorted Gaussians per block, one per thread
-constexpr int kCW = 4, kCIt = 8;        // segment ranking: 4 waves x 8 items
-constexpr int kCSeg = kCW * 64 * kCIt;  // 2048 segments ranked per round
+constexpr int kCW = 4, kCIt = 8;        // segment ranking: 4 waves x up to 8 items
+constexpr int kCSeg = kCW * 64 * kCIt;  // up to 2048 segments ranked per round
 static_assert(kCG == kRadixBins, "one thread per column in the column scans");
+
+struct ColScatterSmem {
+    uint32_t x0w[kCG], y0h[kCG], id[kCG], seg0[kCG + 1];
+    uint32_t colbase[kRadixBins], colw0[kRadixBins];
+    uint32_t keys[kCSeg], vals[kCSeg];  // the round's segments by column
+    uint32_t wpre[kCSeg + 1];           // pair offset of each sorted segment
+    uint32_t tmp[4];
+};
+
+// One round of k_col_scatter: segments [R, R + rn) of the block, ranked kIt per lane (rn <=
+// 256 kIt; blocks with few segments take the smaller instantiation, whose ranking pass costs
+// half as much).
+template <int kIt, typename Smem>
+__device__ __forceinline__ void col_round(uint32_t R, uint32_t rn, int pack_shift,
+                                          uint32_t *__restrict__ out, ColScatterSmem &c, Smem &sm) {
+    constexpr int kSeg = kCW * 64 * kIt;
+    const int tid = threadIdx.x;
+    uint32_t k[kIt], v[kIt];
+#pragma unroll
+    for (int j = 0; j < kIt; ++j) {
+        const uint32_t slot = (uint32_t)((tid >> 6) * (kSeg / kCW) + j * 64 + (tid & 63));
+        k[j] = 0xFFFFFFFFu;  // padding: largest column, after every real segment
+        v[j] = 0u;
+        if (slot < rn) {
+            const uint32_t sg = R + slot;
+            int lo = 0, hi = kCG - 1;  // last Gaussian whose first segment is <= sg
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (c.seg0[mid] <= sg) lo = mid;
+                else hi = mid - 1;
+            }
+            k[j] = (c.x0w[lo] & 0xFFFFu) + (sg - c.seg0[lo]);
+            v[j] = (uint32_t)lo;
+        }
+    }
+    radix_tile_scatter<kCW, kIt, false, false>(k, v, (int)rn, 0, 8, nullptr, 0, 0, nullptr,
+                                               nullptr, nullptr, sm, c.keys, c.vals);
+    // pair offsets of the sorted segments (heights, exclusive prefix)
+    uint32_t hh[kIt], hsum = 0;
+#pragma unroll
+    for (int j = 0; j < kIt; ++j) {
+        const uint32_t p = (uint32_t)(tid * kIt + j);
+        hh[j] = p < rn ? c.y0h[c.vals[p]] >> 16 : 0u;
+        hsum += hh[j];
+    }
+    uint32_t npairs;
+    uint32_t pre = block256_exclusive_scan(hsum, c.tmp, npairs);
+#pragma unroll
+    for (int j = 0; j < kIt; ++j) {
+        c.wpre[tid * kIt + j] = pre;
+        pre += hh[j];
+    }
+    if (tid == 0) c.wpre[kSeg] = npairs;
+    __syncthreads();
+    c.colw0[tid] = sm.count[tid] ? c.wpre[sm.delta[tid]] : 0u;
+    __syncthreads();
+    // one thread per sorted segment (consecutive lanes: consecutive segments, so within a
+    // column consecutive destination runs); each writes its h pairs
+    for (uint32_t p = tid; p < rn; p += kCG) {
+        const uint32_t col = c.keys[p], t = c.vals[p];
+        const uint32_t y0h = c.y0h[t], id = c.id[t];
+        const uint32_t dst = c.colbase[col] + (c.wpre[p] - c.colw0[col]);
+        const uint32_t y0 = y0h & 0xFFFFu, h = y0h >> 16;
+        for (uint32_t r = 0; r < h; ++r)
+            out[dst + r] = (pack_shift < 32 ? (y0 + r) << pack_shift : 0u) | id;
+    }
+    __syncthreads();  // every thread has read this round's column bases
+    // the next round continues every column where this one ended
+    if (sm.count[tid]) c.colbase[tid] += c.wpre[sm.delta[tid] + sm.count[tid]] - c.colw0[tid];
+    __syncthreads();
+}
 
 __global__ __launch_bounds__(kCG) void k_col_count(const uint32_t *__restrict__ perm,
                                                    const uint2 *__restrict__ strip_rect,
@@ -423,12 +494,11 @@ __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict_
                                                      const uint32_t *__restrict__ hist, int64_t nb,
                                                      const uint32_t *__restrict__ digit_total,
                                                      int pack_shift, uint32_t *__restrict__ out) {
-    __shared__ uint32_t s_x0w[kCG], s_y0h[kCG], s_id[kCG], s_seg0[kCG + 1];
-    __shared__ uint32_t s_colbase[kRadixBins], s_colw0[kRadixBins];
-    __shared__ uint32_t s_keys[kCSeg], s_vals[kCSeg];  // the round's segments by column
-    __shared__ uint32_t s_wpre[kCSeg + 1];              // pair offset of each sorted segment
-    __shared__ RadixTileSmem<kCW, kCIt> sm;
-    __shared__ uint32_t s_tmp[4];
+    __shared__ ColScatterSmem c;
+    __shared__ union {
+        RadixTileSmem<kCW, kCIt> big;
+        RadixTileSmem<kCW, kCIt / 2> small;
+    } sm;
     const int tid = threadIdx.x;
     const int64_t n = *d_n;
     const int64_t base = (int64_t)blockIdx.x * kCG;
@@ -436,74 +506,25 @@ __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict_
     const int64_t e = base + tid;
     const bool valid = e < n;
     const uint2 r = valid ? rect_sorted[e] : make_uint2(0u, 0u);
-    s_x0w[tid] = r.x;
-    s_y0h[tid] = r.y;
-    s_id[tid] = valid ? perm[e] : 0u;
+    c.x0w[tid] = r.x;
+    c.y0h[tid] = r.y;
+    c.id[tid] = valid ? perm[e] : 0u;
     uint32_t tot;
     // global start of column d for this block: all earlier columns, then earlier blocks
-    const uint32_t dstart = block256_exclusive_scan(digit_total[tid], s_tmp, tot);
-    s_colbase[tid] = dstart + hist[(int64_t)tid * nb + blockIdx.x];
+    const uint32_t dstart = block256_exclusive_scan(digit_total[tid], c.tmp, tot);
+    c.colbase[tid] = dstart + hist[(int64_t)tid * nb + blockIdx.x];
     // thread t owns segments [seg0, seg0 + w) (one per column of its rect)
     uint32_t nseg;
-    const uint32_t seg0 = block256_exclusive_scan(r.x >> 16, s_tmp, nseg);
-    s_seg0[tid] = seg0;
-    if (tid == 0) s_seg0[kCG] = nseg;
+    const uint32_t seg0 = block256_exclusive_scan(r.x >> 16, c.tmp, nseg);
+    c.seg0[tid] = seg0;
+    if (tid == 0) c.seg0[kCG] = nseg;
     __syncthreads();
     for (uint32_t R = 0; R < nseg; R += kCSeg) {
         const uint32_t rn = min((uint32_t)kCSeg, nseg - R);
-        uint32_t k[kCIt], v[kCIt];
-#pragma unroll
-        for (int j = 0; j < kCIt; ++j) {
-            const uint32_t slot = (uint32_t)((tid >> 6) * (kCSeg / kCW) + j * 64 + (tid & 63));
-            k[j] = 0xFFFFFFFFu;  // padding: largest column, after every real segment
-            v[j] = 0u;
-            if (slot < rn) {
-                const uint32_t sg = R + slot;
-                int lo = 0, hi = kCG - 1;  // last Gaussian whose first segment is <= sg
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (s_seg0[mid] <= sg) lo = mid;
-                    else hi = mid - 1;
-                }
-                k[j] = (s_x0w[lo] & 0xFFFFu) + (sg - s_seg0[lo]);
-                v[j] = (uint32_t)lo;
-            }
-        }
-        radix_tile_scatter<kCW, kCIt, false, false>(k, v, (int)rn, 0, 8, nullptr, 0, 0, nullptr,
-                                                    nullptr, nullptr, sm, s_keys, s_vals);
-        // pair offsets of the sorted segments (heights, exclusive prefix)
-        uint32_t hh[kCIt], hsum = 0;
-#pragma unroll
-        for (int j = 0; j < kCIt; ++j) {
-            const uint32_t p = (uint32_t)(tid * kCIt + j);
-            hh[j] = p < rn ? s_y0h[s_vals[p]] >> 16 : 0u;
-            hsum += hh[j];
-        }
-        uint32_t npairs;
-        uint32_t pre = block256_exclusive_scan(hsum, s_tmp, npairs);
-#pragma unroll
-        for (int j = 0; j < kCIt; ++j) {
-            s_wpre[tid * kCIt + j] = pre;
-            pre += hh[j];
-        }
-        if (tid == 0) s_wpre[kCSeg] = npairs;
-        __syncthreads();
-        s_colw0[tid] = sm.count[tid] ? s_wpre[sm.delta[tid]] : 0u;
-        __syncthreads();
-        // one thread per sorted segment (consecutive lanes: consecutive segments, so within a
-        // column consecutive destination runs); each writes its h pairs
-        for (uint32_t p = tid; p < rn; p += kCG) {
-            const uint32_t c = s_keys[p], t = s_vals[p];
-            const uint32_t y0h = s_y0h[t], id = s_id[t];
-            const uint32_t dst = s_colbase[c] + (s_wpre[p] - s_colw0[c]);
-            const uint32_t y0 = y0h & 0xFFFFu, h = y0h >> 16;
-            for (uint32_t r = 0; r < h; ++r)
-                out[dst + r] = (pack_shift < 32 ? (y0 + r) << pack_shift : 0u) | id;
-        }
-        __syncthreads();  // every thread has read this round's column bases
-        // the next round continues every column where this one ended
-        if (sm.count[tid]) s_colbase[tid] += s_wpre[sm.delta[tid] + sm.count[tid]] - s_colw0[tid];
-        __syncthreads();
+        if (rn <= (uint32_t)kCSeg / 2)
+            col_round<kCIt / 2>(R, rn, pack_shift, out, c, sm.small);
+        else
+            col_round<kCIt>(R, rn, pack_shift, out, c, sm.big);
     }
 }
 
