@@ -113,10 +113,10 @@ class Scene:
 # tools/profile.sh + tools/prof_summary.py --json) of the default configuration, and the kernel
 # each stage's roofline refers to.  The bench cannot read PMC counters itself; the profile is
 # of this same command (c3, default options).
-TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r01_c3_v11_kernels.json")
-STAGE_KERNEL = {"blend": "k_blend_q<true", "preprocess": "k_preprocess<false>",
+TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r02_c3_kernels.json")
+STAGE_KERNEL = {"blend": "k_blend_q<true, false>", "preprocess": "k_preprocess<false>",
                 "color": "k_color", "depth_sort": None, "duplicate": "k_col_scatter",
-                "tile_sort": None, "scan": None, "ranges": "k_ranges"}
+                "tile_sort": None, "scan": None, "ranges": None}
 
 
 def measured_traffic(stage, config, default_opts):

@@ -151,7 +151,7 @@ int reserve_P(gsr_context *ctx, int64_t P, hipStream_t s) {
     GSR_TRY(grow(ctx, ctx->ds_b, n * 8, s));
     GSR_TRY(grow(ctx, ctx->partials, (size_t)std::max<int64_t>(gsr_scan_blocks(P), 1) * 4, s));
     GSR_TRY(grow_zeroed(ctx, ctx->total, 16, s));  // [K (u64), look-back error flag (u32)]
-    GSR_TRY(grow(ctx, ctx->pair_count, 256 * 16, s));  // k_count_pairs: 256 blocks x (8 + 8 B)
+    GSR_TRY(grow(ctx, ctx->pair_count, 1024 * 16, s));  // k_count_pairs: 1024 blocks x (8 + 8 B)
     GSR_TRY(grow(ctx, ctx->hist, (size_t)std::max(gsr_radix_hist_words(P),
                                                   gsr_depth_sort_hist_words(P)) * 4, s));
     // column-first binning's per-(block, column) counts: its own buffer, since reserve_K may

@@ -792,10 +792,13 @@ hipError_t gsr_launch_tile_ranges_aux(const uint2 *strip_rect, int64_t P, uint32
         if (e != hipSuccess) return e;
         attr_done.fetch_or(bit, std::memory_order_release);
     }
-    hipLaunchKernelGGL(k_tile_diff, dim3(kTileDiffBlocks), dim3(kDiffThreads), lds, s, strip_rect,
-                       P, gx, rows, partial);
+    // one block per 16k rects (at least 64, at most kTileDiffBlocks): the rect pass stays
+    // short at 6M Gaussians while the finalize's sum over the partials stays small at 1M
+    const int nparts = (int)std::min<int64_t>(kTileDiffBlocks, std::max<int64_t>(64, (P + 16383) / 16384));
+    hipLaunchKernelGGL(k_tile_diff, dim3(nparts), dim3(kDiffThreads), lds, s, strip_rect, P, gx,
+                       rows, partial);
     hipLaunchKernelGGL(k_tile_finalize, dim3(rows), dim3(kFinThreads), 0, s, partial,
-                       kTileDiffBlocks, gx, rows, ranges);
+                       nparts, gx, rows, ranges);
     return hipGetLastError();
 }
 

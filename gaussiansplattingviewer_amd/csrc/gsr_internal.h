@@ -213,7 +213,7 @@ struct GsrPreprocessArgs {
     // per Gaussian: strip-clipped tile rect {x0 | width << 16, strip-local row0 | rows << 16},
     // {0, 0} when it has no pair in the strip (grid dimensions < 2^16, checked by the host)
     uint2 *strip_rect;
-    // per k_count_pairs block (256): its (Gaussian, strip tile) pair count, then 256 uint2 of
+    // per k_count_pairs block (1024): its (Gaussian, strip tile) pair count, then 1024 uint2 of
     // the OR / AND of its kept depth keys
     uint64_t *block_pairs;
     unsigned long long *host_K;  // pinned host memory (device-mapped): [K, D] of this frame
@@ -330,9 +330,9 @@ hipError_t gsr_launch_ranges(const uint32_t *tile_keys, int64_t K, uint32_t *ran
                              hipStream_t s);
 // Tile ranges from the Gaussians' strip tile rects alone (no sorted keys): per-tile pair
 // counts via per-row difference arrays, then an exclusive scan; runs on the second stream.
-// partial: kTileDiffBlocks * cells words, cells = gsr_tile_diff_cells(...) <= kTileDiffMaxCells
+// partial: kTileDiffBlocks * cells words (capacity), cells = gsr_tile_diff_cells(...) <= kTileDiffMaxCells
 // (the difference arrays live in LDS).
-constexpr int kTileDiffBlocks = 64;
+constexpr int kTileDiffBlocks = 256;  // at most; 64 up to 1M Gaussians, more for more
 constexpr uint32_t kTileDiffMaxCells = 38912;  // 152 KiB of LDS
 // (gx + 1) column-difference cells per tile row, then rows + 1 row-width differences
 __host__ __device__ inline uint32_t gsr_tile_diff_cells(uint32_t gx, uint32_t rows) {

@@ -409,8 +409,9 @@ __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
 // K and the depth keys' bit span for the host, on the second stream right after the
 // preprocess: per-block sums of the (Gaussian, strip tile) pair counts from the packed strip
 // rects, and the OR / AND of the depth keys of the Gaussians with pairs (the sort keys the
-// depth sort keeps), grid-stride over 256 blocks.
-constexpr int kCountBlocks = 256;
+// depth sort keeps), grid-stride over up to 1024 blocks (at 6M Gaussians 256 blocks left the
+// pass latency-bound: 105 us on a C4 strip).
+constexpr int kCountBlocks = 1024;
 __global__ __launch_bounds__(256) void k_count_pairs(const uint2 *__restrict__ strip_rect,
                                                      const uint32_t *__restrict__ keys, int64_t P,
                                                      unsigned long long *__restrict__ block_pairs,
