@@ -4,6 +4,7 @@
 // gsr_forward replaces upstream `_C.rasterize_gaussians` / Rasterizer::forward
 // (rasterizer_impl.cu), which the viewer reaches through renderer_cuda.py:211-224.
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -47,6 +48,7 @@ struct gsr_context {
     DevBuf records, strip_rect, sort_keys, partials, total, hist, digit_total, bin, chunk_first,
         rect_sorted, pair_count;
     DevBuf ds_a, ds_b;  // depth sort: (key, id) pairs between passes (ping-pong)
+    DevBuf block_kept;  // depth sort compaction (strips): kept keys per 256-Gaussian block
     DevBuf perm;    // the depth sort's result: Gaussian ids in depth order (kept ones)
     DevBuf ds_ctl;  // depth sort control words: kept count, key bits, per-tile key stats
     DevBuf col_hist;  // column-first binning: per-(Gaussian block, column) pair counts
@@ -55,8 +57,11 @@ struct gsr_context {
     DevBuf ranges_local;
     DevBuf tile_diff;  // difference-array partials of the second-stream tile ranges
     // pinned: [K from the device scan (debug), unused, K from the pair count, depth key bits D]
+    // [4]: (frame tag << 32) | D from the depth sort's pass 0
     uint64_t *h_total = nullptr;
     unsigned long long *d_hostK = nullptr;  // device view of h_total + 2
+    unsigned long long *d_hostD = nullptr;  // device view of h_total + 4
+    uint32_t sort_tag = 0;                  // frames sorted on this context (tags h_total[4])
     hipEvent_t kcount_ready = nullptr;  // the pair counts of this frame are on the host
     // state of the last forward (for gsr_get_binning)
     bool have_forward = false;
@@ -91,6 +96,12 @@ struct gsr_context {
     bool serial_color = false; // tuning (env GSR_SERIAL_COLOR): join right after the fork
     bool late_K = false;       // tuning (env GSR_LATE_K): also sync on the scan's total
     bool split_color = true;   // GSR_OPT_SPLIT_COLOR
+    // depth sort compaction (GSR_OPT_COMPACT_SORT, env GSR_COMPACT_SORT): 1 on, 0 off, -1 auto
+    // = on for strips of >= 4M Gaussians.  A strip keeps a fraction of the Gaussians; compacting
+    // them first spares pass 0 the dropped keys (C4 1/8 strip: 2,017 -> 2,097 fps), but it
+    // delays the pass-0 D the host waits for, which costs more than it saves on small frames
+    // (C3 1/8 strip: 9,290 -> 7,170 fps with two frames in flight)
+    int compact_sort = -1;
     // Stage timing: a ring of event sets, one per forward, read back after the timed region.
     int timing = 0;  // 0 off, 1 every stage, 2 the blend only, on every 8th forward
     int64_t forwards = 0;  // forwards since gsr_set_timing (mode 2's sampling)
@@ -149,6 +160,7 @@ int reserve_P(gsr_context *ctx, int64_t P, hipStream_t s) {
     GSR_TRY(grow(ctx, ctx->sort_keys, n * 4, s));
     GSR_TRY(grow(ctx, ctx->ds_a, n * 8, s));
     GSR_TRY(grow(ctx, ctx->ds_b, n * 8, s));
+    GSR_TRY(grow(ctx, ctx->block_kept, 4 * ((n + 255) / 256), s));
     GSR_TRY(grow(ctx, ctx->partials, (size_t)std::max<int64_t>(gsr_scan_blocks(P), 1) * 4, s));
     GSR_TRY(grow_zeroed(ctx, ctx->total, 16, s));  // [K (u64), look-back error flag (u32)]
     GSR_TRY(grow(ctx, ctx->pair_count, 1024 * 16, s));  // k_count_pairs: 1024 blocks x (8 + 8 B)
@@ -204,14 +216,17 @@ int gsr_create(gsr_context **out) {
         delete ctx;
         return fail(GSR_E_HIP, "gsr_create: no HIP device");
     }
-    if (hipHostMalloc(reinterpret_cast<void **>(&ctx->h_total), 4 * sizeof(uint64_t),
+    if (hipHostMalloc(reinterpret_cast<void **>(&ctx->h_total), 6 * sizeof(uint64_t),
                       hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->d_hostK), ctx->h_total + 2, 0) !=
+            hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->d_hostD), ctx->h_total + 4, 0) !=
             hipSuccess) {
         (void)hipGetLastError();
         delete ctx;
         return fail(GSR_E_HIP, "gsr_create: hipHostMalloc failed");
     }
+    std::memset(ctx->h_total, 0, 6 * sizeof(uint64_t));  // tag 0 never matches a frame
     int prio_least = 0, prio_greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) {
         (void)hipGetLastError();
@@ -227,6 +242,8 @@ int gsr_create(gsr_context **out) {
     if (env_pp) ctx->packed_pairs = std::atoi(env_pp);
     const char *env_ar = std::getenv("GSR_AUX_RANGES");
     if (env_ar) ctx->aux_ranges = std::atoi(env_ar);
+    const char *env_cs = std::getenv("GSR_COMPACT_SORT");
+    if (env_cs) ctx->compact_sort = std::atoi(env_cs);
     const char *env_xg = std::getenv("GSR_BLEND_XCD_GROUP");
     if (env_xg) ctx->blend_xcd_group = (uint32_t)std::atoi(env_xg);
     ctx->serial_color = std::getenv("GSR_SERIAL_COLOR") != nullptr;
@@ -257,7 +274,7 @@ void gsr_destroy(gsr_context *ctx) {
     if (!ctx) return;
     (void)hipDeviceSynchronize();
     DevBuf *bufs[] = {&ctx->records,       &ctx->strip_rect,    &ctx->sort_keys,
-                      &ctx->ds_a,          &ctx->ds_b,
+                      &ctx->ds_a,          &ctx->ds_b,          &ctx->block_kept,
                       &ctx->partials,      &ctx->total,         &ctx->hist,
                       &ctx->digit_total,   &ctx->bin,           &ctx->chunk_first,
                       &ctx->rect_sorted,   &ctx->pair_count,    &ctx->perm,
@@ -314,6 +331,11 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
     }
     if (option == GSR_OPT_PACKED_PAIRS) {
         ctx->packed_pairs = value ? 1 : 0;
+        return GSR_OK;
+    }
+    if (option == GSR_OPT_COMPACT_SORT) {
+        if (value < -1 || value > 1) return fail(GSR_E_INVALID, "gsr_set_option: compact -1..1");
+        ctx->compact_sort = (int)value;
         return GSR_OK;
     }
     if (option == GSR_OPT_TILE_SORT_SHAPE) {
@@ -484,6 +506,9 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     pa.radii = out->radii;
     pa.records = static_cast<gsr::SplatRecord *>(ctx->records.p);
     pa.sort_keys = static_cast<uint32_t *>(ctx->sort_keys.p);
+    const bool compact_sort =
+        ctx->compact_sort < 0 ? (rows_tiles < gy && P >= (4 << 20)) : ctx->compact_sort != 0;
+    pa.block_kept = compact_sort ? static_cast<uint32_t *>(ctx->block_kept.p) : nullptr;
     pa.strip_rect = static_cast<uint2 *>(ctx->strip_rect.p);
     pa.block_pairs = static_cast<uint64_t *>(ctx->pair_count.p);
     pa.host_K = ctx->d_hostK;
@@ -549,32 +574,37 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     uint32_t *d_valid = static_cast<uint32_t *>(ctx->ds_ctl.p);
     uint32_t *perm = static_cast<uint32_t *>(ctx->perm.p);
     uint2 *ds_a = static_cast<uint2 *>(ctx->ds_a.p), *ds_b = static_cast<uint2 *>(ctx->ds_b.p);
-    GSR_HIP(gsr_depth_sort(pa.sort_keys, P, 1, ds_a, ds_b, perm, hist, digit_total, d_valid, 0, 1,
-                           s),
-            "depth sort launch");
-    // K (the pair count, which sizes the binning) and D (the bits in which the kept depth keys
-    // differ) come from the second stream's pair count, published in pinned memory ~10 us after
-    // the preprocess -- before pass 0 ends, so the host learns how many more passes the sort
-    // needs and queues them without idling the GPU
-    uint64_t K = 0;
+    // compacted keys / ids live in ds_b until pass 1 overwrites it
+    uint32_t *keys_c = reinterpret_cast<uint32_t *>(ds_b), *ids_c = keys_c + P;
+    const uint32_t tag = ++ctx->sort_tag;
+    auto depth_sort = [&](int p0, int p1) {
+        return compact_sort
+                   ? gsr_depth_sort_compacted(pa.sort_keys, P, pa.block_kept, keys_c, ids_c, ds_a,
+                                              ds_b, perm, hist, digit_total, d_valid, p0, p1, s,
+                                              ctx->d_hostD, tag)
+                   : gsr_depth_sort(pa.sort_keys, P, 1, ds_a, ds_b, perm, hist, digit_total,
+                                    d_valid, p0, p1, s, ctx->d_hostD, tag);
+    };
+    GSR_HIP(depth_sort(0, 1), "depth sort launch");
+    // D (the bits in which the kept depth keys differ) arrives in pinned memory from pass 0's
+    // scan, tagged with this frame, while pass 0's downsweep runs: the host then queues only the
+    // passes D needs before the GPU reaches them.  If it does not arrive in 50 ms (a GPU still
+    // busy with earlier frames), all passes are queued and the unneeded ones exit at once.
     int depth_passes = 3;
-    if (split_color) {
-        GSR_HIP(hipEventSynchronize(ctx->kcount_ready), "hipEventSynchronize(pair count)");
-        K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
-        depth_passes = gsr_depth_sort_passes((uint32_t)ctx->h_total[3]);
+    {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t spin = 0;; ++spin) {
+            const uint64_t v = __atomic_load_n(&ctx->h_total[4], __ATOMIC_ACQUIRE);
+            if ((uint32_t)(v >> 32) == tag) {
+                depth_passes = gsr_depth_sort_passes((uint32_t)v);
+                break;
+            }
+            if ((spin & 1023u) == 1023u &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
+                break;
+        }
     }
-    GSR_HIP(gsr_depth_sort(pa.sort_keys, P, 1, ds_a, ds_b, perm, hist, digit_total, d_valid, 1,
-                           depth_passes, s),
-            "depth sort launch");
-    if (dbg && split_color) {  // the device's own D (pass 0) must agree with the published one
-        uint32_t ctl2[2];
-        GSR_HIP(hipMemcpyAsync(ctl2, d_valid, 8, hipMemcpyDeviceToHost, s), "hipMemcpyAsync(ctl)");
-        GSR_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(ctl)");
-        if (ctl2[1] != (uint32_t)ctx->h_total[3])
-            return fail(GSR_E_HIP, "gsr_forward: depth key bits mismatch (pair count " +
-                                       std::to_string(ctx->h_total[3]) + ", sort " +
-                                       std::to_string(ctl2[1]) + ")");
-    }
+    GSR_HIP(depth_sort(1, depth_passes), "depth sort launch");
     GSR_TRY(stage_end(1));
 
     // ---- 3. offsets scan over depth-sorted strip tile counts; K readback --------------------
@@ -604,6 +634,24 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         GSR_HIP(hipMemcpyAsync(ctx->h_total, d_total, 16, hipMemcpyDeviceToHost, s),
                 "hipMemcpyAsync(num_rendered)");
     GSR_TRY(stage_end(2));
+    // K (the pair count, which sizes the binning) from the second stream's pair count,
+    // published in pinned memory ~20 us after the preprocess; the host waits for it only after
+    // the sort and the column counts are queued
+    uint64_t K = 0;
+    if (split_color) {
+        GSR_HIP(hipEventSynchronize(ctx->kcount_ready), "hipEventSynchronize(pair count)");
+        K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
+        if (dbg) {  // the pair count's D and the sort's own D (pass 0) agree
+            uint32_t ctl2[2];
+            GSR_HIP(hipMemcpyAsync(ctl2, d_valid, 8, hipMemcpyDeviceToHost, s),
+                    "hipMemcpyAsync(ctl)");
+            GSR_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(ctl)");
+            if (ctl2[1] != (uint32_t)ctx->h_total[3])
+                return fail(GSR_E_HIP, "gsr_forward: depth key bits mismatch (pair count " +
+                                           std::to_string(ctx->h_total[3]) + ", sort " +
+                                           std::to_string(ctl2[1]) + ")");
+        }
+    }
     if (check_device_total) {
         GSR_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(num_rendered)");
         if (!split_color) K = ctx->h_total[0];

@@ -9,9 +9,10 @@
 //   * pass 0's upsweep also reduces the OR and the AND of the kept keys.  Bits where they agree
 //     are equal in every key, so only the low D = bits_for(OR ^ AND) bits need sorting: at C3
 //     every depth lies in [2, 6) (keys 0x40000000..0x40BFFFFF, D = 24) and two passes do.
-//     The forward learns D on the host with K (k_count_pairs / k_publish_K compute it on the
-//     second stream) and launches only the needed passes; callers that do not know D launch
-//     all three and the unneeded ones exit at once (the kernels read D from ctl).  The last
+//     Pass 0's scan also stores D, tagged with the frame, into pinned host memory; the forward
+//     waits for it while pass 0's downsweep runs and launches only the needed passes.  Callers
+//     that do not wait launch all three and the unneeded ones exit at once (the kernels read D
+//     from ctl).  The last
 //     needed pass writes the permutation straight to `perm`;
 //   * compaction: pass 0 drops the sentinel keys (0xFFFFFFFF: Gaussians without pairs in the
 //     strip) and stores the kept count on the device; later passes read it.
@@ -55,10 +56,11 @@ template <bool kFirst>
 __global__ __launch_bounds__(kDThreads) void k_ds_upsweep(const void *__restrict__ in,
                                                           int64_t n_host, int drop,
                                                           uint32_t *__restrict__ ctl, int shift,
-                                                          uint32_t *__restrict__ hist) {
+                                                          uint32_t *__restrict__ hist,
+                                                          const uint32_t *__restrict__ d_n) {
     __shared__ uint32_t s_h[kDBins];
     __shared__ uint32_t s_red[3][kDW];
-    int64_t n = n_host;
+    int64_t n = d_n ? (int64_t)*d_n : n_host;  // d_n: the compacted count (first pass)
     if (!kFirst) {
         if (ctl[1] <= (uint32_t)shift) return;  // constant digit: pass skipped
         n = ctl[0];
@@ -147,10 +149,12 @@ constexpr int kScanDigits = 16, kScanGroups = 16, kScanReg = 8;
 template <bool kFirst>
 __global__ __launch_bounds__(256) void k_ds_scan(uint32_t *__restrict__ hist, int64_t n_host,
                                                  uint32_t *__restrict__ ctl, int shift,
-                                                 uint32_t *__restrict__ digit_total) {
+                                                 uint32_t *__restrict__ digit_total,
+                                                 const uint32_t *__restrict__ d_n,
+                                                 unsigned long long *host_D, uint32_t tag) {
     __shared__ uint32_t s_sum[kScanGroups][kScanDigits];
     __shared__ uint32_t s_red[3][4];
-    int64_t n = n_host;
+    int64_t n = d_n ? (int64_t)*d_n : n_host;
     if (!kFirst) {
         if (ctl[1] <= (uint32_t)shift) return;
         n = ctl[0];
@@ -227,8 +231,14 @@ __global__ __launch_bounds__(256) void k_ds_scan(uint32_t *__restrict__ hist, in
                 c += s_red[2][i];
             }
             const uint32_t diff = c ? (o ^ a) : 0u;
+            const uint32_t D = diff ? 32u - (uint32_t)__clz(diff) : 0u;
             ctl[0] = c;
-            ctl[1] = diff ? 32u - (uint32_t)__clz(diff) : 0u;
+            ctl[1] = D;
+            // D for the host, tagged with the frame (pinned memory, system scope): it launches
+            // only the passes D needs, while this pass's downsweep runs
+            if (host_D)
+                __hip_atomic_store(host_D, ((unsigned long long)tag << 32) | D, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
@@ -292,19 +302,20 @@ __device__ __forceinline__ int tile_rank_scatter(const uint32_t (&k)[kDIt],
     return (int)total;
 }
 
-// kFirst: `in` is the n keys and the values are the element indices; else `in` is the
+// kFirst: `in` is the n keys and the values are the element indices (or ids_in[e]); else `in` is the
 // previous pass's (key, id) pairs.  last (decided from D on the device): write only the ids,
 // to perm; else the (key, id) pairs to pairs_out.
 template <bool kFirst>
 __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
     const void *__restrict__ in, uint2 *__restrict__ pairs_out, uint32_t *__restrict__ perm,
     int64_t n_host, int drop, const uint32_t *__restrict__ ctl, int shift,
-    const uint32_t *__restrict__ hist, const uint32_t *__restrict__ digit_total) {
+    const uint32_t *__restrict__ hist, const uint32_t *__restrict__ digit_total,
+    const uint32_t *__restrict__ ids_in, const uint32_t *__restrict__ d_n) {
     __shared__ uint32_t s_keys[kDT], s_vals[kDT], s_tab[kDBins];  // 48 KiB
     __shared__ uint32_t s_wcnt[kDSubBins * kDW];
     __shared__ uint32_t s_tmp[kDW];
     const uint32_t D = ctl[1];
-    int64_t n = n_host;
+    int64_t n = d_n ? (int64_t)*d_n : n_host;
     if (!kFirst) {
         if (D <= (uint32_t)shift) return;
         n = ctl[0];
@@ -323,7 +334,7 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
         const bool valid = e < n;
         if (kFirst) {
             k[j] = valid ? static_cast<const uint32_t *>(in)[e] : 0u;
-            v[j] = (uint32_t)e;
+            v[j] = (ids_in && valid) ? ids_in[e] : (uint32_t)e;
         } else {
             const uint2 q = valid ? static_cast<const uint2 *>(in)[e] : make_uint2(0u, 0u);
             k[j] = q.x;
@@ -408,6 +419,49 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
     }
 }
 
+// Compacting front end: exclusive scan of the per-256-block kept counts in place (one block),
+// total -> ctl[0].
+__global__ __launch_bounds__(1024) void k_ds_compact_scan(uint32_t *__restrict__ block_kept,
+                                                          int64_t nb, uint32_t *__restrict__ ctl) {
+    __shared__ uint32_t s_tmp[16];
+    const int tid = threadIdx.x;
+    const int64_t per = (nb + 1023) / 1024, b0 = tid * per, b1 = min(nb, b0 + per);
+    uint32_t sum = 0;
+    for (int64_t b = b0; b < b1; ++b) sum += block_kept[b];
+    uint32_t total;
+    uint32_t pre = blockw_exclusive_scan<16>(sum, s_tmp, total);
+    for (int64_t b = b0; b < b1; ++b) {
+        const uint32_t c = block_kept[b];
+        block_kept[b] = pre;
+        pre += c;
+    }
+    if (tid == 0) ctl[0] = total;
+}
+
+// Block b (256 keys): its kept keys (not 0xFFFFFFFF), in order, to keys_c / ids_c from offset
+// block_off[b].
+__global__ __launch_bounds__(256) void k_ds_compact(const uint32_t *__restrict__ keys, int64_t n,
+                                                    const uint32_t *__restrict__ block_off,
+                                                    uint32_t *__restrict__ keys_c,
+                                                    uint32_t *__restrict__ ids_c) {
+    __shared__ uint32_t s_w[4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t idx = (int64_t)blockIdx.x * 256 + tid;
+    const uint32_t key = idx < n ? keys[idx] : kDropKey;
+    const bool keep = key != kDropKey;
+    const uint64_t bal = __ballot(keep);
+    if (lane == 0) s_w[w] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t base = block_off[blockIdx.x];
+    for (int i = 0; i < w; ++i) base += s_w[i];
+    if (keep) {
+        const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+        const uint32_t dst = base + (uint32_t)__popcll(bal & lt);
+        keys_c[dst] = key;
+        ids_c[dst] = (uint32_t)idx;
+    }
+}
+
 }  // namespace
 
 int64_t gsr_depth_sort_hist_words(int64_t n) {
@@ -423,12 +477,10 @@ int gsr_depth_sort_passes(uint32_t key_bits) {
     return key_bits <= (uint32_t)kDBits ? 1 : key_bits <= (uint32_t)(2 * kDBits) ? 2 : kDPasses;
 }
 
-hipError_t gsr_depth_sort(const uint32_t *keys, int64_t n, int drop, uint2 *pairs_a,
-                          uint2 *pairs_b, uint32_t *perm, uint32_t *hist, uint32_t *digit_total,
-                          uint32_t *ctl, int pass_begin, int pass_end, hipStream_t s) {
-    if (n <= 0 || pass_begin >= pass_end) return hipSuccess;
-    if (n > (int64_t)UINT32_MAX || pass_begin < 0 || pass_end > kDPasses)
-        return hipErrorInvalidValue;
+static hipError_t ds_passes(const uint32_t *keys, const uint32_t *ids_in, const uint32_t *d_n,
+                            int64_t n, int drop, uint2 *pairs_a, uint2 *pairs_b, uint32_t *perm,
+                            uint32_t *hist, uint32_t *digit_total, uint32_t *ctl, int pass_begin,
+                            int pass_end, unsigned long long *host_D, uint32_t tag, hipStream_t s) {
     const unsigned nt = (unsigned)((n + kDT - 1) / kDT);
     const void *in[kDPasses] = {keys, pairs_a, pairs_b};
     uint2 *out[kDPasses] = {pairs_a, pairs_b, nullptr};
@@ -436,19 +488,50 @@ hipError_t gsr_depth_sort(const uint32_t *keys, int64_t n, int drop, uint2 *pair
         const int shift = p * kDBits;
         if (p == 0) {
             hipLaunchKernelGGL(k_ds_upsweep<true>, dim3(nt), dim3(kDThreads), 0, s, in[p], n, drop,
-                               ctl, shift, hist);
+                               ctl, shift, hist, d_n);
             hipLaunchKernelGGL(k_ds_scan<true>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist,
-                               n, ctl, shift, digit_total);
+                               n, ctl, shift, digit_total, d_n, host_D, tag);
             hipLaunchKernelGGL(k_ds_downsweep<true>, dim3(nt), dim3(kDThreads), 0, s, in[p], out[p],
-                               perm, n, drop, ctl, shift, hist, digit_total);
+                               perm, n, drop, ctl, shift, hist, digit_total, ids_in, d_n);
         } else {
             hipLaunchKernelGGL(k_ds_upsweep<false>, dim3(nt), dim3(kDThreads), 0, s, in[p], n, 0,
-                               ctl, shift, hist);
+                               ctl, shift, hist, nullptr);
             hipLaunchKernelGGL(k_ds_scan<false>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist,
-                               n, ctl, shift, digit_total);
+                               n, ctl, shift, digit_total, nullptr, nullptr, 0u);
             hipLaunchKernelGGL(k_ds_downsweep<false>, dim3(nt), dim3(kDThreads), 0, s, in[p],
-                               out[p], perm, n, 0, ctl, shift, hist, digit_total);
+                               out[p], perm, n, 0, ctl, shift, hist, digit_total, nullptr, nullptr);
         }
     }
     return hipGetLastError();
+}
+
+hipError_t gsr_depth_sort(const uint32_t *keys, int64_t n, int drop, uint2 *pairs_a,
+                          uint2 *pairs_b, uint32_t *perm, uint32_t *hist, uint32_t *digit_total,
+                          uint32_t *ctl, int pass_begin, int pass_end, hipStream_t s,
+                          unsigned long long *host_D, uint32_t tag) {
+    if (n <= 0 || pass_begin >= pass_end) return hipSuccess;
+    if (n > (int64_t)UINT32_MAX || pass_begin < 0 || pass_end > kDPasses)
+        return hipErrorInvalidValue;
+    return ds_passes(keys, nullptr, nullptr, n, drop, pairs_a, pairs_b, perm, hist, digit_total,
+                     ctl, pass_begin, pass_end, host_D, tag, s);
+}
+
+hipError_t gsr_depth_sort_compacted(const uint32_t *keys, int64_t n, uint32_t *block_kept,
+                                    uint32_t *keys_c, uint32_t *ids_c, uint2 *pairs_a,
+                                    uint2 *pairs_b, uint32_t *perm, uint32_t *hist,
+                                    uint32_t *digit_total, uint32_t *ctl, int pass_begin,
+                                    int pass_end, hipStream_t s, unsigned long long *host_D,
+                                    uint32_t tag) {
+    if (n <= 0 || pass_begin >= pass_end) return hipSuccess;
+    if (n > (int64_t)UINT32_MAX || pass_begin < 0 || pass_end > kDPasses)
+        return hipErrorInvalidValue;
+    if (pass_begin == 0) {
+        const int64_t nb = (n + 255) / 256;
+        hipLaunchKernelGGL(k_ds_compact_scan, dim3(1), dim3(1024), 0, s, block_kept, nb, ctl);
+        hipLaunchKernelGGL(k_ds_compact, dim3((unsigned)nb), dim3(256), 0, s, keys, n, block_kept,
+                           keys_c, ids_c);
+    }
+    // the passes read the compacted count from ctl[0] (grids sized for n)
+    return ds_passes(keys_c, ids_c, ctl, n, 0, pairs_a, pairs_b, perm, hist, digit_total, ctl,
+                     pass_begin, pass_end, host_D, tag, s);
 }

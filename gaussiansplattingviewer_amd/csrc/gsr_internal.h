@@ -210,6 +210,7 @@ struct GsrPreprocessArgs {
     int32_t *radii;
     gsr::SplatRecord *records;
     uint32_t *sort_keys;  // depth keys (0xFFFFFFFF: no pair in the strip); values are indices
+    uint32_t *block_kept; // optional: per 256-Gaussian block, its count of kept keys
     // per Gaussian: strip-clipped tile rect {x0 | width << 16, strip-local row0 | rows << 16},
     // {0, 0} when it has no pair in the strip (grid dimensions < 2^16, checked by the host)
     uint2 *strip_rect;
@@ -275,9 +276,22 @@ int64_t gsr_depth_sort_hist_words(int64_t n);
 int64_t gsr_depth_sort_ctl_words(int64_t n);
 int gsr_depth_sort_digit_words();
 int gsr_depth_sort_passes(uint32_t key_bits);
+// host_D (optional, device view of pinned host memory): pass 0 stores (tag << 32) | D there.
 hipError_t gsr_depth_sort(const uint32_t *keys, int64_t n, int drop, uint2 *pairs_a,
                           uint2 *pairs_b, uint32_t *perm, uint32_t *hist, uint32_t *digit_total,
-                          uint32_t *ctl, int pass_begin, int pass_end, hipStream_t s);
+                          uint32_t *ctl, int pass_begin, int pass_end, hipStream_t s,
+                          unsigned long long *host_D = nullptr, uint32_t tag = 0);
+// Compacting front end for sparse key sets (strips): the kept keys of each 256-key block
+// (block_kept[b] of them, from the preprocess) are written in order to keys_c, their indices
+// to ids_c, and their count to ctl[0]; then the sort runs on those (gsr_depth_sort_compacted,
+// same contract as gsr_depth_sort with drop, n the uncompacted upper bound).  block_kept is
+// scanned in place.  keys_c / ids_c may be the two halves of pairs_b.
+hipError_t gsr_depth_sort_compacted(const uint32_t *keys, int64_t n, uint32_t *block_kept,
+                                    uint32_t *keys_c, uint32_t *ids_c, uint2 *pairs_a,
+                                    uint2 *pairs_b, uint32_t *perm, uint32_t *hist,
+                                    uint32_t *digit_total, uint32_t *ctl, int pass_begin,
+                                    int pass_end, hipStream_t s,
+                                    unsigned long long *host_D = nullptr, uint32_t tag = 0);
 
 // Binning: offsets scan over depth-sorted strip tile counts, duplicate into (tile, id)
 // pairs, and tile ranges.

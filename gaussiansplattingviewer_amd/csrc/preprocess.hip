@@ -286,11 +286,19 @@ __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, i
     return strip_tiles;
 }
 
-// One thread per Gaussian.
+// One thread per Gaussian.  With a.block_kept (the depth sort's compaction, strips): block b
+// also stores how many of its 256 Gaussians have pairs in the strip.
 template <bool kColor>
 __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx < a.P) preprocess_one<kColor>(a, idx);
+    const bool kept = idx < a.P && preprocess_one<kColor>(a, idx) != 0u;
+    if (a.block_kept) {
+        __shared__ uint32_t s_cnt[4];
+        const uint32_t c = (uint32_t)__popcll(__ballot(kept));
+        if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) a.block_kept[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    }
 }
 
 // One block, after k_count_pairs on the second stream (the kernel boundary makes its stores

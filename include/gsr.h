@@ -222,9 +222,15 @@ const char *gsr_stage_name(int i);
  *     array count and a segment scatter -- instead of regenerating and ranking every pair; the
  *     second pass sorts packed (tile row, Gaussian id) words.  Needs the second-stream ranges,
  *     <= 256 tile columns and rows per strip, P <= 2^(32 - row bits).  Identical results. */
+/*   GSR_OPT_COMPACT_SORT (default -1 = auto): 1 = the depth sort first compacts the keys of
+ *     the Gaussians with pairs in the strip (per-block counts from the preprocess, a scan, an
+ *     ordered scatter) and sorts only those; 0 = pass 0 drops the others while it sorts; auto =
+ *     compact on strips (tile_row_begin/end a proper subset) of >= 4M Gaussians, where most
+ *     keys are dropped and pass 0 is long.  Identical results. */
 enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2,
        GSR_OPT_TILE_SORT_SHAPE = 4, GSR_OPT_FUSED_BINNING = 5,
-       GSR_OPT_SPLIT_COLOR = 8, GSR_OPT_PACKED_PAIRS = 9, GSR_OPT_COLUMN_PAIRS = 10 };
+       GSR_OPT_SPLIT_COLOR = 8, GSR_OPT_PACKED_PAIRS = 9, GSR_OPT_COLUMN_PAIRS = 10,
+       GSR_OPT_COMPACT_SORT = 11 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
 
 #ifdef __cplusplus

@@ -269,6 +269,7 @@ VARIANTS = {  # [(option, alternative value, default), ...]
     "tile_shape0": [(_lib.GSR_OPT_TILE_SORT_SHAPE, 0, 3)],
     "tile_shape5": [(_lib.GSR_OPT_TILE_SORT_SHAPE, 5, 3)],
     "no_cull": [(_lib.GSR_OPT_BLEND_CULL, 0, 1)],
+    "compact_sort": [(_lib.GSR_OPT_COMPACT_SORT, 1, -1)],
     "inline_color": [(_lib.GSR_OPT_SPLIT_COLOR, 0, 1)],
     "inline_color_unfused": [(_lib.GSR_OPT_SPLIT_COLOR, 0, 1), (_lib.GSR_OPT_FUSED_BINNING, 0, 1)],
 }
@@ -308,7 +309,7 @@ def test_sort_implementations_agree(gpu, variant, size):
         np.testing.assert_array_equal(alt[k], ref[k], err_msg=k)
 
 
-@pytest.mark.parametrize("variant", ["default", "per_pair", "unpacked", "unfused"])
+@pytest.mark.parametrize("variant", ["default", "per_pair", "unpacked", "unfused", "compact_sort"])
 def test_long_tile_lists_and_depth_ties(gpu, oracle_mod, variant):
     """Tiles covered by more than 2048 splats (multi-chunk digit runs in the tile sort, long
     blend lists) and half of the Gaussians at one depth (ties: upstream orders them by
@@ -325,21 +326,28 @@ def test_long_tile_lists_and_depth_ties(gpu, oracle_mod, variant):
     assert_parity(hip, orc)
 
 
+@pytest.mark.parametrize("compact", [0, 1])
 @pytest.mark.parametrize("spread", [0.0, 2e-4, 0.05, 1.5, 60.0])
-def test_depth_sort_pass_regimes(gpu, oracle_mod, spread):
+def test_depth_sort_pass_regimes(gpu, oracle_mod, spread, compact):
     """The depth sort (depth_sort.hip) sorts only the key bits that differ between the kept
     Gaussians' depths (D = bits of OR ^ AND), in 12-bit passes decided on the device: all
     depths equal (D = 0), within 2^12 ulps (one pass), within 2^24 (two passes: 2.5..2.55, and
     2.5..4 across a float exponent) and 2.5..62.5 (three passes, five exponents).  25k Gaussians
-    = 4 sort tiles; off-screen ones are dropped by pass 0 (sentinel keys)."""
+    = 4 sort tiles; off-screen ones are dropped by pass 0 (sentinel keys), or compacted away
+    first (GSR_OPT_COMPACT_SORT)."""
     g = synthetic_gaussians(25000, 3, 31)
     rng = np.random.default_rng(31)
+    _set_option(gpu, _lib.GSR_OPT_COMPACT_SORT, compact)
     g.xyz[:, 2] = (np.float32(0.5) - rng.random(25000, dtype=np.float32) * np.float32(spread))
     g.xyz[::5, 2] = g.xyz[1::5, 2]  # ties across tiles
     s = scene_inputs(g, static_camera(320, 240, (0, 0, 3.0)), 3)
     orc = run_oracle(oracle_mod, s)
     assert orc["num_rendered"] > 0
-    assert_parity(run_hip(s, gpu), orc)
+    try:
+        hip = run_hip(s, gpu)
+    finally:
+        _set_option(gpu, _lib.GSR_OPT_COMPACT_SORT, -1)
+    assert_parity(hip, orc)
 
 
 def test_tile_lists_of_one_depth(gpu, oracle_mod):

@@ -53,17 +53,17 @@ int main() {
         for (int p = 0; p < 3; ++p) {  // pass 2 exits at once (D = 24)
             const int shift = p * 12;
             if (p == 0) {
-                hipLaunchKernelGGL(k_ds_upsweep<true>, dim3(nt), dim3(kDThreads), 0, s, in[p], n, 1, ctl, shift, hist);
+                hipLaunchKernelGGL(k_ds_upsweep<true>, dim3(nt), dim3(kDThreads), 0, s, in[p], n, 1, ctl, shift, hist, nullptr);
                 hipEventRecord(ev[q++], s);
-                hipLaunchKernelGGL(k_ds_scan<true>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist, n, ctl, shift, dt);
+                hipLaunchKernelGGL(k_ds_scan<true>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist, n, ctl, shift, dt, nullptr, nullptr, 0u);
                 hipEventRecord(ev[q++], s);
-                hipLaunchKernelGGL(k_ds_downsweep<true>, dim3(nt), dim3(kDThreads), 0, s, in[p], out[p], perm, n, 1, ctl, shift, hist, dt);
+                hipLaunchKernelGGL(k_ds_downsweep<true>, dim3(nt), dim3(kDThreads), 0, s, in[p], out[p], perm, n, 1, ctl, shift, hist, dt, nullptr, nullptr);
             } else {
-                hipLaunchKernelGGL(k_ds_upsweep<false>, dim3(nt), dim3(kDThreads), 0, s, in[p], n, 0, ctl, shift, hist);
+                hipLaunchKernelGGL(k_ds_upsweep<false>, dim3(nt), dim3(kDThreads), 0, s, in[p], n, 0, ctl, shift, hist, nullptr);
                 hipEventRecord(ev[q++], s);
-                hipLaunchKernelGGL(k_ds_scan<false>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist, n, ctl, shift, dt);
+                hipLaunchKernelGGL(k_ds_scan<false>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist, n, ctl, shift, dt, nullptr, nullptr, 0u);
                 hipEventRecord(ev[q++], s);
-                hipLaunchKernelGGL(k_ds_downsweep<false>, dim3(nt), dim3(kDThreads), 0, s, in[p], out[p], perm, n, 0, ctl, shift, hist, dt);
+                hipLaunchKernelGGL(k_ds_downsweep<false>, dim3(nt), dim3(kDThreads), 0, s, in[p], out[p], perm, n, 0, ctl, shift, hist, dt, nullptr, nullptr);
             }
             hipEventRecord(ev[q++], s);
         }
