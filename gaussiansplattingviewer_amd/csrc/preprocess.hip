@@ -199,6 +199,18 @@ __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, i
 
     const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1],
                                  a.means3D[3 * idx + 2]);
+    // every per-Gaussian input is loaded up front, so all loads are in flight together instead
+    // of a second round trip after the frustum test (they are needed for every Gaussian in
+    // the frustum: all of them at C3)
+    float3 s_in = make_float3(0.f, 0.f, 0.f);
+    float4 q_in = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (!a.cov3D_precomp) {
+        s_in = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+        q_in = a.rot_vec4 ? reinterpret_cast<const float4 *>(a.rotations)[idx]
+                          : make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1],
+                                        a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
+    }
+    const float opacity_in = a.opacities[idx];
     const float3 p_view = transform_point_4x3(p, a.viewmatrix);
     if (p_view.z > 0.2f) {  // in_frustum
         const float4 p_hom = transform_point_4x4(p, a.projmatrix);
@@ -210,12 +222,7 @@ __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, i
 #pragma unroll
             for (int i = 0; i < 6; ++i) cov3d[i] = a.cov3D_precomp[6 * idx + i];
         } else {
-            const float3 s = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1],
-                                         a.scales[3 * idx + 2]);
-            const float4 q = a.rot_vec4 ? reinterpret_cast<const float4 *>(a.rotations)[idx]
-                                        : make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1],
-                                                      a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
-            compute_cov3d(s, a.scale_modifier, q, cov3d);
+            compute_cov3d(s_in, a.scale_modifier, q_in, cov3d);
         }
         const float3 cov = compute_cov2d(p_view, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy,
                                          cov3d, a.viewmatrix);
@@ -233,7 +240,7 @@ __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, i
             const Rect rc = get_rect(px, py, r_int, a.grid_x, a.grid_y);
             all_tiles = (rc.x1 - rc.x0) * (rc.y1 - rc.y0);
             if (all_tiles != 0) {
-                const float opacity = a.opacities[idx];
+                const float opacity = opacity_in;
                 radius_out = r_int;
                 const uint32_t sy0 = max(rc.y0, a.row_begin), sy1 = min(rc.y1, a.row_end);
                 strip_tiles = sy1 > sy0 ? (rc.x1 - rc.x0) * (sy1 - sy0) : 0u;
