@@ -530,9 +530,39 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
             if (!done) (void)hipStreamWaitEvent(s, join, 0);
         }
     } join_guard{s, ctx->join};
+    // fork point of the second stream (colour, K, tile ranges): right after the preprocess.  Its
+    // work is queued after the depth sort's first pass, so the host hands the critical chain to
+    // the GPU first (queueing ~10 second-stream commands first left the main queue idle ~40 us
+    // on a strip frame, where the host's submission rate is the bound)
+    if (split_color) GSR_HIP(hipEventRecord(ctx->fork, s), "hipEventRecord(fork)");
+    if (!split_color && tmode == 1) {  // no colour stage: record an empty interval
+        GSR_HIP(hipEventRecord(evc[0], s), "hipEventRecord");
+        GSR_HIP(hipEventRecord(evc[1], s), "hipEventRecord");
+    }
+    GSR_TRY(stage_end(0));
+
+    // ---- 2. stable sort of the Gaussians by view depth (depth_sort.hip) -------------------
+    // compacting: Gaussians without pairs in the strip (sentinel keys) are dropped by the first
+    // pass; the count of the rest lands in ds_ctl[0] (device), the pass count is decided there
+    uint32_t *hist = static_cast<uint32_t *>(ctx->hist.p);
+    uint32_t *digit_total = static_cast<uint32_t *>(ctx->digit_total.p);
+    uint32_t *d_valid = static_cast<uint32_t *>(ctx->ds_ctl.p);
+    uint32_t *perm = static_cast<uint32_t *>(ctx->perm.p);
+    uint2 *ds_a = static_cast<uint2 *>(ctx->ds_a.p), *ds_b = static_cast<uint2 *>(ctx->ds_b.p);
+    // compacted keys / ids live in ds_b until pass 1 overwrites it
+    uint32_t *keys_c = reinterpret_cast<uint32_t *>(ds_b), *ids_c = keys_c + P;
+    const uint32_t tag = ++ctx->sort_tag;
+    auto depth_sort = [&](int p0, int p1) {
+        return compact_sort
+                   ? gsr_depth_sort_compacted(pa.sort_keys, P, pa.block_kept, keys_c, ids_c, ds_a,
+                                              ds_b, perm, hist, digit_total, d_valid, p0, p1, s,
+                                              ctx->d_hostD, tag)
+                   : gsr_depth_sort(pa.sort_keys, P, 1, ds_a, ds_b, perm, hist, digit_total,
+                                    d_valid, p0, p1, s, ctx->d_hostD, tag);
+    };
+    GSR_HIP(depth_sort(0, 1), "depth sort launch");
     if (split_color) {
-        // fork: colour on the second stream, overlapped with the depth sort and the binning
-        GSR_HIP(hipEventRecord(ctx->fork, s), "hipEventRecord(fork)");
+        // second stream: colour, overlapped with the depth sort and the binning
         GSR_HIP(hipStreamWaitEvent(ctx->aux, ctx->fork, 0), "hipStreamWaitEvent(fork)");
         // K (the pair count) first: k_count_pairs + k_publish_K store it into pinned memory;
         // the host waits for it only after the depth sort and the scan are enqueued, so the
@@ -560,32 +590,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         join_guard.done = false;
         if (dbg) GSR_HIP(hipStreamSynchronize(ctx->aux), "stage color");
         if (ctx->serial_color) GSR_HIP(hipStreamWaitEvent(s, ctx->join, 0), "hipStreamWaitEvent");
-    } else if (tmode == 1) {  // no colour stage: record an empty interval
-        GSR_HIP(hipEventRecord(evc[0], s), "hipEventRecord");
-        GSR_HIP(hipEventRecord(evc[1], s), "hipEventRecord");
     }
-    GSR_TRY(stage_end(0));
-
-    // ---- 2. stable sort of the Gaussians by view depth (depth_sort.hip) -------------------
-    // compacting: Gaussians without pairs in the strip (sentinel keys) are dropped by the first
-    // pass; the count of the rest lands in ds_ctl[0] (device), the pass count is decided there
-    uint32_t *hist = static_cast<uint32_t *>(ctx->hist.p);
-    uint32_t *digit_total = static_cast<uint32_t *>(ctx->digit_total.p);
-    uint32_t *d_valid = static_cast<uint32_t *>(ctx->ds_ctl.p);
-    uint32_t *perm = static_cast<uint32_t *>(ctx->perm.p);
-    uint2 *ds_a = static_cast<uint2 *>(ctx->ds_a.p), *ds_b = static_cast<uint2 *>(ctx->ds_b.p);
-    // compacted keys / ids live in ds_b until pass 1 overwrites it
-    uint32_t *keys_c = reinterpret_cast<uint32_t *>(ds_b), *ids_c = keys_c + P;
-    const uint32_t tag = ++ctx->sort_tag;
-    auto depth_sort = [&](int p0, int p1) {
-        return compact_sort
-                   ? gsr_depth_sort_compacted(pa.sort_keys, P, pa.block_kept, keys_c, ids_c, ds_a,
-                                              ds_b, perm, hist, digit_total, d_valid, p0, p1, s,
-                                              ctx->d_hostD, tag)
-                   : gsr_depth_sort(pa.sort_keys, P, 1, ds_a, ds_b, perm, hist, digit_total,
-                                    d_valid, p0, p1, s, ctx->d_hostD, tag);
-    };
-    GSR_HIP(depth_sort(0, 1), "depth sort launch");
     // D (the bits in which the kept depth keys differ) arrives in pinned memory from pass 0's
     // scan, tagged with this frame, while pass 0's downsweep runs: the host then queues only the
     // passes D needs before the GPU reaches them.  If it does not arrive in 50 ms (a GPU still

@@ -420,22 +420,51 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
 }
 
 // Compacting front end: exclusive scan of the per-256-block kept counts in place (one block),
-// total -> ctl[0].
+// total -> ctl[0].  Rounds of 16k counts: each thread owns 16 consecutive counts (four 16-B
+// loads issued together, a wave covers 4 KB contiguous), one block scan per round.  (A strided
+// per-thread serial loop was 47 us at 6M Gaussians: ~23 dependent loads per thread.)
 __global__ __launch_bounds__(1024) void k_ds_compact_scan(uint32_t *__restrict__ block_kept,
                                                           int64_t nb, uint32_t *__restrict__ ctl) {
+    constexpr int kR = 4, kPer = 4 * kR;
     __shared__ uint32_t s_tmp[16];
     const int tid = threadIdx.x;
-    const int64_t per = (nb + 1023) / 1024, b0 = tid * per, b1 = min(nb, b0 + per);
-    uint32_t sum = 0;
-    for (int64_t b = b0; b < b1; ++b) sum += block_kept[b];
-    uint32_t total;
-    uint32_t pre = blockw_exclusive_scan<16>(sum, s_tmp, total);
-    for (int64_t b = b0; b < b1; ++b) {
-        const uint32_t c = block_kept[b];
-        block_kept[b] = pre;
-        pre += c;
+    uint32_t carry = 0;
+    for (int64_t base = 0; base < nb; base += 1024 * kPer) {
+        const int64_t e0 = base + (int64_t)tid * kPer;
+        uint32_t c[kPer];
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+            const int64_t e = e0 + 4 * r;
+            if (e + 3 < nb) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(block_kept + e);
+                c[4 * r] = v.x, c[4 * r + 1] = v.y, c[4 * r + 2] = v.z, c[4 * r + 3] = v.w;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) c[4 * r + q] = e + q < nb ? block_kept[e + q] : 0u;
+            }
+        }
+        uint32_t sum = 0;
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) sum += c[q];
+        uint32_t total;
+        uint32_t pre = carry + blockw_exclusive_scan<16>(sum, s_tmp, total);
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+            const int64_t e = e0 + 4 * r;
+            uint32_t o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = pre, pre += c[4 * r + q];
+            if (e + 3 < nb) {
+                *reinterpret_cast<uint4 *>(block_kept + e) = make_uint4(o[0], o[1], o[2], o[3]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (e + q < nb) block_kept[e + q] = o[q];
+            }
+        }
+        carry += total;
     }
-    if (tid == 0) ctl[0] = total;
+    if (tid == 0) ctl[0] = carry;
 }
 
 // Block b (256 keys): its kept keys (not 0xFFFFFFFF), in order, to keys_c / ids_c from offset
