@@ -91,6 +91,10 @@ struct gsr_context {
     // blocks); 256 the best serial frame (0.369 vs 0.386 ms): the colour then takes fewer CUs
     // from the depth sort it overlaps (env GSR_COLOR_BLOCKS)
     int color_blocks = 0;
+    // k_color: colour waves per SIMD (0 = as many as fit; -1 = auto: 3 below 4M Gaussians, else
+    // 4 -- GSR_COLOR_WAVES sweeps on MI355X, C3 and a C4 strip)
+    int color_waves = -1;
+    bool wait_D = true;  // host learns D before queueing the depth sort's later passes
     uint32_t blend_xcd_group = 16;  // tuning (env GSR_BLEND_XCD_GROUP)
     int aux_low_priority = 1;  // second stream at the lowest priority
     bool serial_color = false; // tuning (env GSR_SERIAL_COLOR): join right after the fork
@@ -236,6 +240,8 @@ int gsr_create(gsr_context **out) {
     ctx->aux_low_priority = env_prio ? std::atoi(env_prio) : 1;
     const char *env_cb = std::getenv("GSR_COLOR_BLOCKS");    // tuning: grid cap, 0 = none
     if (env_cb) ctx->color_blocks = std::atoi(env_cb);
+    const char *env_cw = std::getenv("GSR_COLOR_WAVES");     // tuning: 0 = no cap
+    if (env_cw) ctx->color_waves = std::atoi(env_cw);
     const char *env_cp = std::getenv("GSR_COLUMN_PAIRS");
     if (env_cp) ctx->column_pairs = std::atoi(env_cp);
     const char *env_pp = std::getenv("GSR_PACKED_PAIRS");
@@ -247,6 +253,8 @@ int gsr_create(gsr_context **out) {
     const char *env_xg = std::getenv("GSR_BLEND_XCD_GROUP");
     if (env_xg) ctx->blend_xcd_group = (uint32_t)std::atoi(env_xg);
     ctx->serial_color = std::getenv("GSR_SERIAL_COLOR") != nullptr;
+    const char *env_wd = std::getenv("GSR_WAIT_D");  // tuning: 0 = queue every pass at once
+    if (env_wd) ctx->wait_D = std::atoi(env_wd) != 0;
     ctx->late_K = std::getenv("GSR_LATE_K") != nullptr;
     bool ok = hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking,
                                           ctx->aux_low_priority ? prio_least : 0) == hipSuccess &&
@@ -576,7 +584,9 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
                                                static_cast<uint2 *>(ctx->ranges_local.p), ctx->aux),
                     "tile ranges launch");
         }
-        GSR_HIP(gsr_launch_color(pa, ctx->color_blocks, ctx->aux), "color launch");
+        GSR_HIP(gsr_launch_color(pa, ctx->color_blocks,
+                                 ctx->color_waves >= 0 ? ctx->color_waves : P < (4 << 20) ? 3 : 4,
+                                 ctx->aux), "color launch");
         if (aux_ranges && ctx->aux_ranges != 1) {
             uint32_t *part = static_cast<uint32_t *>(ctx->tile_diff.p);
             GSR_HIP(gsr_launch_tile_ranges_aux(pa.strip_rect, P, gx, rows_tiles, part,
@@ -596,7 +606,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     // passes D needs before the GPU reaches them.  If it does not arrive in 50 ms (a GPU still
     // busy with earlier frames), all passes are queued and the unneeded ones exit at once.
     int depth_passes = 3;
-    {
+    if (ctx->wait_D) {
         const auto t0 = std::chrono::steady_clock::now();
         for (uint32_t spin = 0;; ++spin) {
             const uint64_t v = __atomic_load_n(&ctx->h_total[4], __ATOMIC_ACQUIRE);

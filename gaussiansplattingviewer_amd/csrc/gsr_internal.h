@@ -227,7 +227,9 @@ struct GsrPreprocessArgs {
 hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, bool with_color, hipStream_t s);
 // SH -> RGB (or colors_precomp) of every Gaussian with radii > 0 into SplatRecord.c.yzw (+ rgb)
 // max_blocks > 0 caps the grid (grid-stride loop).
-hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, hipStream_t s);
+// waves_per_simd (1..7): cap on the colour waves a CU holds at once (0 = no cap).
+hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, int waves_per_simd,
+                            hipStream_t s);
 // K of the frame (sum of the strip rects' pair counts) -> *a.host_K (pinned host memory).
 hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s);
 hipError_t gsr_launch_mark_visible(const float *means3D, int64_t P, const float *viewmatrix,

@@ -397,14 +397,18 @@ __device__ __forceinline__ void store_color(const GsrPreprocessArgs &a, int64_t 
 }
 
 // Degree 3 with 16-B aligned rows (the host launches k_color_generic otherwise), grid-stride
-// over waves of 64 Gaussians (the grid may be capped so the colour pass, which runs beside the
-// latency-bound depth sort on the second stream, leaves CUs free for it; uncapped by default).
-// Every lane that needs a colour reads its own 192-B row with 12 x 16-B loads -- a wave's 64
-// rows are 12 KiB contiguous, so its 12 load instructions hit the same lines and each line
-// leaves L2 once -- and consumes the coefficients as they arrive (eval_sh3_stream).  An LDS
-// transpose of the wave's rows (coalesced loads, 13 KiB of LDS per wave, 130 VGPRs) was
-// slower: 144 vs 83 us per launch at the same grid cap (C3, interleaved A/B on MI355X).
+// over waves of 64 Gaussians.  Every lane that needs a colour reads its own 192-B row with 12 x
+// 16-B loads and consumes the coefficients as they arrive (eval_sh3_stream, upstream's order).
+// A wave's 12 loads touch 64 lines each, and the lines are re-fetched from L2 as the CU's other
+// waves evict them (~8x the row bytes in L2 -> L1 traffic), which the latency-bound depth sort
+// on the main stream feels.  So the launch caps how many colour waves a CU holds
+// (gsr_launch_color's waves_per_simd, through the block's LDS allocation): at C3, 4 per SIMD
+// instead of the 7 the registers allow cut the in-frame depth sort 90 -> 79 us and raised the
+// in-flight frame rate 4.5 %.  Rejected: coalesced loads of the wave's 64 rows
+// through an LDS slab (every line moves L2 -> L1 once, but all 64 rows are read where ~60 % are
+// needed: 3,259 vs 3,400 frames/s); an LDS transpose of all 64 rows at once (144 vs 83 us).
 __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
+    extern __shared__ uint32_t s_occupancy_cap[];  // reserved only to cap blocks per CU
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t n_waves = (a.P + 63) / 64;
     const int64_t wave_stride = (int64_t)gridDim.x * 4;
@@ -419,6 +423,7 @@ __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
                                                 reinterpret_cast<const float4 *>(a.shs) + idx * 12));
         }
     }
+    if (a.P < 0) s_occupancy_cap[threadIdx.x] = 0u;  // never: keeps the allocation referenced
 }
 
 // K and the depth keys' bit span for the host, on the second stream right after the
@@ -508,7 +513,8 @@ hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, bool with_color, hi
     return hipGetLastError();
 }
 
-hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, hipStream_t s) {
+hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, int waves_per_simd,
+                            hipStream_t s) {
     if (a.P == 0) return hipSuccess;
     const unsigned g0 = grid_for(a.P);  // 4 waves of 64 Gaussians per block
     if (!a.sh_vec4 || a.colors_precomp || a.D != 3) {
@@ -516,7 +522,19 @@ hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, hipStrea
         return hipGetLastError();
     }
     const unsigned g = max_blocks > 0 && (unsigned)max_blocks < g0 ? max_blocks : g0;
-    hipLaunchKernelGGL(k_color, dim3(g), dim3(256), 0, s, a);
+    // a 4-wave block puts one wave on each SIMD: w blocks per CU = w waves per SIMD, held by
+    // reserving 1/w of the CU's 160 KiB of LDS per block (1 KiB granules)
+    size_t lds = 0;
+    if (waves_per_simd >= 1 && waves_per_simd < 8) {
+        lds = (size_t)(160 * 1024 / waves_per_simd) & ~(size_t)1023;
+        if (lds > 64 * 1024) {
+            const hipError_t e = hipFuncSetAttribute(
+                reinterpret_cast<const void *>(&k_color),
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+    }
+    hipLaunchKernelGGL(k_color, dim3(g), dim3(256), lds, s, a);
     return hipGetLastError();
 }
 
