@@ -94,7 +94,11 @@ struct gsr_context {
     // k_color: colour waves per SIMD (0 = as many as fit; -1 = auto: 3 below 4M Gaussians, else
     // 4 -- GSR_COLOR_WAVES sweeps on MI355X, C3 and a C4 strip)
     int color_waves = -1;
-    bool wait_D = true;  // host learns D before queueing the depth sort's later passes
+    // host learns D before queueing the depth sort's later passes: 1 / 0, or -1 = auto: only when
+    // the previous frame had >= 4M pairs.  Waiting keeps the empty third pass off the GPU (C3:
+    // 3,480 vs 3,340 frames/s) but holds the host to the GPU's progress, which host-bound small
+    // frames (C2, a C3 strip: ~1M pairs) feel more (7,500 vs 8,000-9,300 frames/s in flight)
+    int wait_D = -1;
     uint32_t blend_xcd_group = 16;  // tuning (env GSR_BLEND_XCD_GROUP)
     int aux_low_priority = 1;  // second stream at the lowest priority
     bool serial_color = false; // tuning (env GSR_SERIAL_COLOR): join right after the fork
@@ -254,7 +258,7 @@ int gsr_create(gsr_context **out) {
     if (env_xg) ctx->blend_xcd_group = (uint32_t)std::atoi(env_xg);
     ctx->serial_color = std::getenv("GSR_SERIAL_COLOR") != nullptr;
     const char *env_wd = std::getenv("GSR_WAIT_D");  // tuning: 0 = queue every pass at once
-    if (env_wd) ctx->wait_D = std::atoi(env_wd) != 0;
+    if (env_wd) ctx->wait_D = std::atoi(env_wd);
     ctx->late_K = std::getenv("GSR_LATE_K") != nullptr;
     bool ok = hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking,
                                           ctx->aux_low_priority ? prio_least : 0) == hipSuccess &&
@@ -606,7 +610,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     // passes D needs before the GPU reaches them.  If it does not arrive in 50 ms (a GPU still
     // busy with earlier frames), all passes are queued and the unneeded ones exit at once.
     int depth_passes = 3;
-    if (ctx->wait_D) {
+    if (ctx->wait_D > 0 || (ctx->wait_D < 0 && ctx->last_K >= (4 << 20))) {
         const auto t0 = std::chrono::steady_clock::now();
         for (uint32_t spin = 0;; ++spin) {
             const uint64_t v = __atomic_load_n(&ctx->h_total[4], __ATOMIC_ACQUIRE);

@@ -13,9 +13,10 @@
 // Skipping splats that provably cannot reach alpha >= 1/255 changes nothing: upstream skips
 // them too (`if (alpha < 1/255) continue`), and n_contrib -- upstream's running `contributor`
 // at the last contributing splat -- is that splat's list position + 1 either way.
-// Arithmetic (GSR_OPT_BLEND_FAST): 1 (default) folds log2(e) and -1/2 into the conic at
-// staging, evaluates the quadratic form with FMA and the exponential with the raw v_exp_f32;
-// 0 keeps upstream's per-pixel operation order (the core of ocml's expf).  Both are within the
+// Arithmetic (GSR_OPT_BLEND_FAST): 1 (default) stages each splat as the exponent's quadratic in
+// the lane's offset from the quadrant centre, with log2(e), -1/2 and log2(opacity) folded in
+// (5 FMA per pixel, then the raw v_exp_f32); 0 keeps upstream's per-pixel operation order (the
+// core of ocml's expf).  Both are within the
 // image tolerance of tests/gpu_helpers.py.
 #include "gsr_internal.h"
 
@@ -75,10 +76,16 @@ __device__ __forceinline__ uint32_t xcd_work(uint32_t b, uint32_t group) {
 }
 
 // One staged splat as the inner loop reads it: three 16-B LDS reads from one address.
+// exact: g = x, y, conic a, conic b; q = conic c, opacity, r, g; e = b, position + 1 (uint bits:
+// upstream's `contributor`), -, -.
+// fast: the exponent as a quadratic in the lane's offset (u, v) from the quadrant centre,
+// log2(opacity) folded in: p = k0 + k1 u + k2 v + k3 u^2 + k4 uv + k5 v^2 (g = k0..k3,
+// q = k4, k5, r, g); e = b, position + 1, the bound p must not exceed (log2(opacity): p > it <=>
+// upstream's power > 0; +inf for a positive-definite conic), -.
 struct StagedSplat {
-    float4 g;  // x, y, conic a, conic b      (fast: prescaled a, b)
-    float4 q;  // conic c, opacity, r, g      (fast: prescaled c)
-    float4 e;  // b, list position + 1 (uint bits: upstream's `contributor`), -, -
+    float4 g;
+    float4 q;
+    float4 e;
 };
 
 // Blocks are mapped XCD-aware (xcd_work).  Only the next chunk's point-list ids are
@@ -105,6 +112,9 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
     const float pfx = (float)px, pfy = (float)py;
+    // fast: the lane's offset from the quadrant centre and its products (exact small values)
+    const float pu = (float)(lane & 7) - 3.5f, pv = (float)(lane >> 3) - 3.5f;
+    const float puu = pu * pu, puv = pu * pv, pvv = pv * pv;
 
     const uint2 range = a.ranges[tile];
     // done carried in the sign of T, as in k_blend
@@ -114,17 +124,19 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
     if (!live_any()) return;
 
     auto composite = [&](const StagedSplat &sp) {
-        const float dx = sp.g.x - pfx, dy = sp.g.y - pfy;
         bool vis, acc, term;
         float test_T;
         if (kFast) {
             // The loop-carried chain is only T -> T (1 - alpha_eff) -> compare -> select:
             // alpha_eff = 0 for an invisible splat (then test_T = T and the weight T - test_T
             // is 0), and a pixel that terminates keeps -|T| (idempotent once done).
-            const float p2 =
-                __builtin_fmaf(dx, __builtin_fmaf(sp.g.z, dx, sp.g.w * dy), sp.q.x * dy * dy);
-            const float alpha = fminf(0.99f, sp.q.y * __builtin_amdgcn_exp2f(p2));
-            vis = !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+            float p2 = __builtin_fmaf(sp.g.y, pu, sp.g.x);
+            p2 = __builtin_fmaf(sp.g.z, pv, p2);
+            p2 = __builtin_fmaf(sp.g.w, puu, p2);
+            p2 = __builtin_fmaf(sp.q.x, puv, p2);
+            p2 = __builtin_fmaf(sp.q.y, pvv, p2);
+            const float alpha = fminf(0.99f, __builtin_amdgcn_exp2f(p2));
+            vis = !(p2 > sp.e.z) && !(alpha < 1.0f / 255.0f);
             // T (1 - alpha) as one fma, T - alpha T; alpha_eff = 0 leaves T exactly
             const float alpha_eff = vis ? alpha : 0.0f;
             test_T = __builtin_fmaf(-T, alpha_eff, T);
@@ -138,6 +150,7 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
             T = lo ? -fabsf(T) : test_T;
             return;
         } else {
+            const float dx = sp.g.x - pfx, dy = sp.g.y - pfy;
             const float power =
                 -0.5f * (sp.g.z * dx * dx + sp.q.x * dy * dy) - sp.g.w * dx * dy;
             const float alpha = fminf(0.99f, sp.q.y * exp_core(power));
@@ -172,14 +185,28 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
         if (keep) {
             StagedSplat st;
             if (kFast) {
+                // exponent log2(e) * (-q/2) = a dx^2 + b dx dy + c dy^2 with dx = ex - u,
+                // dy = ey - v, expanded in (u, v)
                 const float kL2e = 1.4426950408889634f;
-                st.g = make_float4(r.a.x, r.a.y, r.a.z * (-0.5f * kL2e), r.a.w * (-kL2e));
-                st.q = make_float4(r.b.x * (-0.5f * kL2e), r.b.y, r.c.y, r.c.z);
+                const float ca = r.a.z * (-0.5f * kL2e), cb = r.a.w * (-kL2e),
+                            cc = r.b.x * (-0.5f * kL2e);
+                const float ex = r.a.x - (X0 + 3.5f), ey = r.a.y - (Y0 + 3.5f);
+                const float lo = __builtin_amdgcn_logf(r.b.y);  // log2(opacity)
+                const float k0 = __builtin_fmaf(ex, __builtin_fmaf(ca, ex, cb * ey), cc * ey * ey);
+                st.g = make_float4(k0 + lo, __builtin_fmaf(-2.0f * ca, ex, -cb * ey),
+                                   __builtin_fmaf(-cb, ex, -2.0f * cc * ey), ca);
+                st.q = make_float4(cb, cc, r.c.y, r.c.z);
+                // upstream skips power > 0, which a positive-definite conic reaches only through
+                // rounding; the expanded form rounds differently (at a centre that falls on a
+                // pixel it can land just above 0), so the test is kept for the other conics only
+                const bool pd = ca < 0.0f && cc < 0.0f && 4.0f * ca * cc > cb * cb;
+                st.e = make_float4(r.c.w, __uint_as_float(idx - range.x + 1u),
+                                   pd ? __builtin_huge_valf() : lo, 0.0f);
             } else {
                 st.g = r.a;
                 st.q = make_float4(r.b.x, r.b.y, r.c.y, r.c.z);
+                st.e = make_float4(r.c.w, __uint_as_float(idx - range.x + 1u), 0.0f, 0.0f);
             }
-            st.e = make_float4(r.c.w, __uint_as_float(idx - range.x + 1u), 0.0f, 0.0f);
             const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
             const int slot = __popcll(bal & lt);  // compacted in list order
             s_spl[slot] = st;
@@ -187,13 +214,17 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
         int count = __popcll(bal);
         if (count == 0) continue;
         // the compacted slots are the list (no index indirection); an odd count is padded with
-        // an opacity-0 splat in slot `count` (< 64 for an odd count)
+        // an opacity-0 splat in slot `count` (< 64 for an odd count): exact: opacity 0; fast:
+        // exponent 0 against a power bound of -inf (never visible)
         if (count & 1) {
-            if (lane < 12) reinterpret_cast<float *>(&s_spl[count])[lane] = 0.0f;
+            if (lane < 12)
+                reinterpret_cast<float *>(&s_spl[count])[lane] =
+                    (kFast && lane == 10) ? -__builtin_huge_valf() : 0.0f;
             ++count;
         }
         // one wave: its LDS writes above complete before the reads below are served
 
+#if GSR_BLEND_PIPELINED
         auto next2 = [&](int k) { return k + 2 < count ? k + 2 : count - 2; };
         StagedSplat a0 = s_spl[0], a1 = s_spl[1];
         for (int k = 0;;) {
@@ -211,6 +242,13 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
             k += 2;
             if (k >= count) break;
         }
+#else
+        for (int k = 0; k < count; k += 2) {
+            const StagedSplat a0 = s_spl[k], a1 = s_spl[k + 1];
+            composite(a0);
+            composite(a1);
+        }
+#endif
         if (!live_any()) break;
     }
 
