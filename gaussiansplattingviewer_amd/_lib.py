@@ -23,6 +23,7 @@ GSR_OPT_SPLIT_COLOR = 8
 GSR_OPT_PACKED_PAIRS = 9
 GSR_OPT_COLUMN_PAIRS = 10
 GSR_OPT_COMPACT_SORT = 11
+GSR_OPT_GRAPH = 12
 
 # Symbols include/gsr.h declares (checked by the CPU test suite).
 EXPORTED_SYMBOLS = (

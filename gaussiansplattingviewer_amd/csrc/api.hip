@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "gsr.h"
 #include "gsr_internal.h"
@@ -37,6 +38,12 @@ struct DevBuf {
 constexpr int kStages = 7;       // the chain on the caller's stream
 constexpr int kAllStages = 8;    // + "color", on the second stream (overlaps stages 1..5)
 constexpr int kTimingRing = 256;  // frames whose stage events are kept
+// gsr_context::frame words: view 16, proj 16, campos 3 (+1), bg 3 (+1) floats, then the frame
+// tag and the device K / overflow words k_col_scatter writes
+constexpr int kFrameView = 0, kFrameProj = 16, kFrameCampos = 32, kFrameBg = 36, kFrameTag = 40,
+              kFrameK = 41, kFrameWords = 44;
+constexpr size_t kMaxGraphs = 4;
+
 const char *kStageNames[kAllStages] = {"preprocess", "depth_sort", "scan",  "duplicate",
                                        "tile_sort",  "ranges",     "blend", "color"};
 
@@ -120,6 +127,39 @@ struct gsr_context {
     // before the blend
     hipStream_t aux = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    // Captured frames (GSR_OPT_GRAPH, env GSR_GRAPH; off by default): the whole forward as
+    // one hipGraph, so a frame costs the host one staging launch + one graph launch (~9 us)
+    // instead of ~20 launches, ~6 event calls and two waits (~100 us).  K is not known when
+    // the graph is built: the pair buffers are sized for graph_cap and the device checks K
+    // against it (k_col_scatter).  Measured on MI355X it does not pay: ROCm replays only
+    // linear graphs as pre-built packet batches (a fork / join graph took 63-115 us to launch,
+    // tools/micro/host_cost), and a linear frame gives up the second stream's overlap (C3:
+    // 3,050 vs 3,510 frames/s; C2 and C3 strips even; small frames are bound by the GPU's
+    // ~2-4 us per dependent kernel, not by the host).  DESIGN.md.
+    int graph = 0;
+    bool capturing = false;     // forward_impl is recording into cap_stream
+    hipStream_t cap_stream = nullptr;
+    DevBuf frame;               // per-frame staging (kFrame* word offsets below)
+    uint32_t frame_tag = 0;     // frames launched as graphs (tags h_total[5])
+    int64_t graph_cap = 0;      // pair capacity of the captured frames (0: not yet known)
+    uint64_t buf_gen = 0;       // bumped by every reallocation (captured pointers go stale)
+    // what a captured frame leaves for gsr_get_binning (set by forward_impl while capturing)
+    uint32_t *cap_point_list = nullptr, *cap_tiles_local = nullptr;
+    uint32_t cap_id_mask = 0xFFFFFFFFu;
+    bool cap_packed = false;
+    struct Graph {
+        std::vector<uint64_t> key;
+        hipGraphExec_t exec = nullptr;
+        uint32_t *point_list = nullptr, *tiles_local = nullptr;
+        uint32_t id_mask = 0xFFFFFFFFu;
+        bool packed = false;
+        uint64_t used = 0;
+    };
+    std::vector<Graph> graphs;  // at most kMaxGraphs, least recently used evicted
+    uint64_t graph_clock = 0;
+    bool graph_stats = false;
+    double gs_acc[3] = {};
+    uint64_t gs_n = 0;
 };
 
 namespace {
@@ -143,6 +183,7 @@ int grow(gsr_context *ctx, DevBuf &b, size_t bytes, hipStream_t s) {
         return fail(GSR_E_NOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
     }
     b.cap = want;
+    ++ctx->buf_gen;
     return GSR_OK;
 }
 
@@ -257,6 +298,9 @@ int gsr_create(gsr_context **out) {
     const char *env_xg = std::getenv("GSR_BLEND_XCD_GROUP");
     if (env_xg) ctx->blend_xcd_group = (uint32_t)std::atoi(env_xg);
     ctx->serial_color = std::getenv("GSR_SERIAL_COLOR") != nullptr;
+    const char *env_gr = std::getenv("GSR_GRAPH");  // 0: every frame on the stream
+    if (env_gr) ctx->graph = std::atoi(env_gr) != 0;
+    ctx->graph_stats = std::getenv("GSR_GRAPH_STATS") != nullptr;
     const char *env_wd = std::getenv("GSR_WAIT_D");  // tuning: 0 = queue every pass at once
     if (env_wd) ctx->wait_D = std::atoi(env_wd);
     ctx->late_K = std::getenv("GSR_LATE_K") != nullptr;
@@ -293,7 +337,9 @@ void gsr_destroy(gsr_context *ctx) {
                       &ctx->ds_ctl,
                       &ctx->tile_keys,     &ctx->tile_vals,
                       &ctx->tile_keys_alt, &ctx->tile_vals_alt, &ctx->ranges_local,
-                      &ctx->tile_diff,     &ctx->col_hist};
+                      &ctx->tile_diff,     &ctx->col_hist,      &ctx->frame};
+    for (auto &e : ctx->graphs) (void)hipGraphExecDestroy(e.exec);
+    if (ctx->cap_stream) (void)hipStreamDestroy(ctx->cap_stream);
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &set : ctx->ev)
@@ -350,6 +396,10 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
         ctx->compact_sort = (int)value;
         return GSR_OK;
     }
+    if (option == GSR_OPT_GRAPH) {
+        ctx->graph = value ? 1 : 0;
+        return GSR_OK;
+    }
     if (option == GSR_OPT_TILE_SORT_SHAPE) {
         if (value < 0 || value > 5) return fail(GSR_E_INVALID, "gsr_set_option: shape 0..5");
         ctx->tile_sort_shape = (int)value;
@@ -397,10 +447,14 @@ int gsr_stage_times(gsr_context *ctx, float *ms, int n) {
     return kAllStages;
 }
 
-int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings *st,
-                gsr_outputs *out, void *stream_) {
-    if (!ctx || !g || !st || !out) return fail(GSR_E_INVALID, "gsr_forward: NULL argument");
-    hipStream_t s = static_cast<hipStream_t>(stream_);
+// The forward on stream s.  ctx->capturing: s is recording a captured frame (gsr_forward):
+// camera and bg come from ctx->frame, K is not waited for (the binning is sized for
+// ctx->graph_cap and reads K on the device) and nothing is published for the host but K.
+static int forward_impl(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings *st,
+                        gsr_outputs *out, hipStream_t s) {
+    const bool cap_mode = ctx->capturing;
+    float *frame = static_cast<float *>(ctx->frame.p);
+    uint32_t *d_K = cap_mode ? reinterpret_cast<uint32_t *>(frame) + kFrameK : nullptr;
     const int64_t P = g->P;
     const int W = st->image_width, H = st->image_height;
     if (P < 0 || P > (int64_t)UINT32_MAX) return fail(GSR_E_INVALID, "gsr_forward: bad P");
@@ -498,9 +552,10 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     pa.shs = g->shs;
     pa.colors_precomp = g->colors_precomp;
     pa.cov3D_precomp = g->cov3D_precomp;
-    pa.viewmatrix = st->viewmatrix;
-    pa.projmatrix = st->projmatrix;
-    pa.campos = st->campos;
+    pa.viewmatrix = cap_mode ? frame + kFrameView : st->viewmatrix;
+    pa.projmatrix = cap_mode ? frame + kFrameProj : st->projmatrix;
+    pa.campos = cap_mode ? (st->campos ? frame + kFrameCampos : nullptr) : st->campos;
+    pa.frame_tag = cap_mode ? reinterpret_cast<const uint32_t *>(frame) + kFrameTag : nullptr;
     pa.tanfovx = st->tanfovx;
     pa.tanfovy = st->tanfovy;
     // rasterizer_impl.cu: focal_y = height / (2.0f * tan_fovy); focal_x likewise (float).
@@ -546,7 +601,9 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     // work is queued after the depth sort's first pass, so the host hands the critical chain to
     // the GPU first (queueing ~10 second-stream commands first left the main queue idle ~40 us
     // on a strip frame, where the host's submission rate is the bound)
-    if (split_color) GSR_HIP(hipEventRecord(ctx->fork, s), "hipEventRecord(fork)");
+    // (a captured frame is one stream: a graph with a fork / join launches ~10x slower on the
+    // host -- ROCm replays only linear graphs as pre-built packet batches, tools/micro/host_cost)
+    if (split_color && !cap_mode) GSR_HIP(hipEventRecord(ctx->fork, s), "hipEventRecord(fork)");
     if (!split_color && tmode == 1) {  // no colour stage: record an empty interval
         GSR_HIP(hipEventRecord(evc[0], s), "hipEventRecord");
         GSR_HIP(hipEventRecord(evc[1], s), "hipEventRecord");
@@ -568,49 +625,59 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         return compact_sort
                    ? gsr_depth_sort_compacted(pa.sort_keys, P, pa.block_kept, keys_c, ids_c, ds_a,
                                               ds_b, perm, hist, digit_total, d_valid, p0, p1, s,
-                                              ctx->d_hostD, tag)
+                                              cap_mode ? nullptr : ctx->d_hostD, tag)
                    : gsr_depth_sort(pa.sort_keys, P, 1, ds_a, ds_b, perm, hist, digit_total,
-                                    d_valid, p0, p1, s, ctx->d_hostD, tag);
+                                    d_valid, p0, p1, s, cap_mode ? nullptr : ctx->d_hostD, tag);
     };
     GSR_HIP(depth_sort(0, 1), "depth sort launch");
     if (split_color) {
         // second stream: colour, overlapped with the depth sort and the binning
-        GSR_HIP(hipStreamWaitEvent(ctx->aux, ctx->fork, 0), "hipStreamWaitEvent(fork)");
+        hipStream_t as = cap_mode ? s : ctx->aux;
+        if (!cap_mode)
+            GSR_HIP(hipStreamWaitEvent(ctx->aux, ctx->fork, 0), "hipStreamWaitEvent(fork)");
         // K (the pair count) first: k_count_pairs + k_publish_K store it into pinned memory;
         // the host waits for it only after the depth sort and the scan are enqueued, so the
         // GPU does not idle on the host round trip
-        GSR_HIP(gsr_launch_count_pairs(pa, ctx->aux), "pair count launch");
-        GSR_HIP(hipEventRecord(ctx->kcount_ready, ctx->aux), "hipEventRecord(pair count)");
-        if (tmode == 1) GSR_HIP(hipEventRecord(evc[0], ctx->aux), "hipEventRecord");
+        GSR_HIP(gsr_launch_count_pairs(pa, as), "pair count launch");
+        if (!cap_mode)
+            GSR_HIP(hipEventRecord(ctx->kcount_ready, as), "hipEventRecord(pair count)");
+        if (tmode == 1) GSR_HIP(hipEventRecord(evc[0], as), "hipEventRecord");
         if (aux_ranges && ctx->aux_ranges == 1) {
             uint32_t *part = static_cast<uint32_t *>(ctx->tile_diff.p);
             GSR_HIP(gsr_launch_tile_ranges_aux(pa.strip_rect, P, gx, rows_tiles, part,
-                                               static_cast<uint2 *>(ctx->ranges_local.p), ctx->aux),
+                                               static_cast<uint2 *>(ctx->ranges_local.p), as),
                     "tile ranges launch");
         }
+        // (in a captured frame the colour runs alone: no cap)
         GSR_HIP(gsr_launch_color(pa, ctx->color_blocks,
-                                 ctx->color_waves >= 0 ? ctx->color_waves : P < (4 << 20) ? 3 : 4,
-                                 ctx->aux), "color launch");
+                                 ctx->color_waves >= 0 ? ctx->color_waves
+                                 : cap_mode            ? 0
+                                 : P < (4 << 20)       ? 3
+                                                       : 4,
+                                 as), "color launch");
         if (aux_ranges && ctx->aux_ranges != 1) {
             uint32_t *part = static_cast<uint32_t *>(ctx->tile_diff.p);
             GSR_HIP(gsr_launch_tile_ranges_aux(pa.strip_rect, P, gx, rows_tiles, part,
-                                               static_cast<uint2 *>(ctx->ranges_local.p), ctx->aux),
+                                               static_cast<uint2 *>(ctx->ranges_local.p), as),
                     "tile ranges launch");
         }
-        if (tmode == 1) GSR_HIP(hipEventRecord(evc[1], ctx->aux), "hipEventRecord");
-        GSR_HIP(hipEventRecord(ctx->join, ctx->aux), "hipEventRecord(join)");
-        // every exit from here on (errors included) leaves the caller's stream behind the
-        // join, so k_color never outlives the caller's view of its inputs
-        join_guard.done = false;
+        if (tmode == 1) GSR_HIP(hipEventRecord(evc[1], as), "hipEventRecord");
+        if (!cap_mode) {
+            GSR_HIP(hipEventRecord(ctx->join, ctx->aux), "hipEventRecord(join)");
+            // every exit from here on (errors included) leaves the caller's stream behind the
+            // join, so k_color never outlives the caller's view of its inputs
+            join_guard.done = false;
+        }
         if (dbg) GSR_HIP(hipStreamSynchronize(ctx->aux), "stage color");
-        if (ctx->serial_color) GSR_HIP(hipStreamWaitEvent(s, ctx->join, 0), "hipStreamWaitEvent");
+        if (ctx->serial_color && !cap_mode)
+            GSR_HIP(hipStreamWaitEvent(s, ctx->join, 0), "hipStreamWaitEvent");
     }
     // D (the bits in which the kept depth keys differ) arrives in pinned memory from pass 0's
     // scan, tagged with this frame, while pass 0's downsweep runs: the host then queues only the
     // passes D needs before the GPU reaches them.  If it does not arrive in 50 ms (a GPU still
     // busy with earlier frames), all passes are queued and the unneeded ones exit at once.
     int depth_passes = 3;
-    if (ctx->wait_D > 0 || (ctx->wait_D < 0 && ctx->last_K >= (4 << 20))) {
+    if (!cap_mode && (ctx->wait_D > 0 || (ctx->wait_D < 0 && ctx->last_K >= (4 << 20)))) {
         const auto t0 = std::chrono::steady_clock::now();
         for (uint32_t spin = 0;; ++spin) {
             const uint64_t v = __atomic_load_n(&ctx->h_total[4], __ATOMIC_ACQUIRE);
@@ -657,7 +724,10 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     // published in pinned memory ~20 us after the preprocess; the host waits for it only after
     // the sort and the column counts are queued
     uint64_t K = 0;
-    if (split_color) {
+    if (cap_mode) {
+        K = (uint64_t)ctx->graph_cap;  // an upper bound; the device knows the real K
+        if (!colpairs) return fail(GSR_E_STATE, "gsr_forward: frame not capturable");
+    } else if (split_color) {
         GSR_HIP(hipEventSynchronize(ctx->kcount_ready), "hipEventSynchronize(pair count)");
         K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
         if (dbg) {  // the pair count's D and the sort's own D (pass 0) agree
@@ -706,7 +776,8 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     if (K > 0 && colpairs) {
         GSR_HIP(gsr_launch_col_pairs_scatter(perm, rect_sorted, P, d_valid,
                                              static_cast<const uint32_t *>(ctx->col_hist.p),
-                                             digit_total, col_shift, tv_alt, s),
+                                             digit_total, col_shift, tv_alt, s,
+                                             cap_mode ? (uint32_t)K : 0xFFFFFFFFu, d_K),
                 "column scatter launch");
         std::swap(tv, tv_alt);
     } else if (K > 0) {
@@ -738,7 +809,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
         if (ybits > 0)
             GSR_HIP(gsr_radix_sort_pairs(&tv, &no_vals, &tv_alt, &no_vals_alt, (int64_t)K,
                                          col_shift, 32, hist, digit_total, s,
-                                         ctx->tile_sort_shape, 0),
+                                         ctx->tile_sort_shape, 0, nullptr, d_K),
                     "tile sort launch");
     } else if (packed) {  // the remaining tile bits of the packed words, keys only
         uint32_t *no_vals = nullptr, *no_vals_alt = nullptr;
@@ -780,7 +851,8 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     ba.rows_tiles = rows_tiles;
     ba.y0 = y0;
     ba.rows_out = rows_out;
-    ba.bg = st->bg;
+    ba.bg = cap_mode ? frame + kFrameBg : st->bg;
+    ba.skip = cap_mode ? d_K + 1 : nullptr;
     ba.out_color = out->color;
     ba.final_T = out->final_T;
     ba.n_contrib = out->n_contrib;
@@ -791,6 +863,13 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     GSR_HIP(gsr_launch_blend(ba, s), "blend launch");
     GSR_TRY(stage_end(6));
 
+    if (cap_mode) {  // gsr_forward publishes these once the frame's K is known
+        ctx->cap_point_list = tv;
+        ctx->cap_tiles_local = tk;
+        ctx->cap_id_mask = id_mask;
+        ctx->cap_packed = packed || colpairs;
+        return GSR_OK;
+    }
     out->num_rendered = (int64_t)K;
     ctx->last_K = (int64_t)K;
     ctx->last_gx = gx; ctx->last_gy = gy; ctx->last_rb = rb; ctx->last_re = re;
@@ -802,6 +881,225 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     ctx->have_forward = true;
     if (tmode) ++ctx->timed_frames;
     return GSR_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Camera, background and frame tag of a captured frame into ctx->frame (one small launch
+// ahead of the graph: the graph's kernels read them from there, so a moving camera -- new
+// tensors every frame -- replays the same graph).
+__global__ void k_stage_frame(const float *__restrict__ view, const float *__restrict__ proj,
+                              const float *__restrict__ campos, const float *__restrict__ bg,
+                              float *__restrict__ frame, uint32_t tag) {
+    const int t = threadIdx.x;
+    if (t < 16)
+        frame[kFrameView + t] = view[t];
+    else if (t < 32)
+        frame[kFrameProj + t - 16] = proj[t - 16];
+    else if (t < 35)
+        frame[kFrameCampos + t - 32] = campos ? campos[t - 32] : 0.0f;
+    else if (t >= 36 && t < 39)
+        frame[kFrameBg + t - 36] = bg[t - 36];
+    else if (t == 40)
+        reinterpret_cast<uint32_t *>(frame)[kFrameTag] = tag;
+}
+
+// Whether forward_impl can record the frame: the column-first binning with second-stream tile
+// ranges, whose kernels all learn K on the device.  (Mirrors forward_impl's own choices.)
+bool capturable(const gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings *st,
+                const gsr_outputs *out) {
+    if (!ctx->graph || ctx->timing != 0 || st->debug || !ctx->split_color || g->P <= 0 ||
+        g->P > (int64_t)UINT32_MAX || !st->viewmatrix || !st->projmatrix || !st->bg ||
+        !out->color || !out->radii || st->image_width <= 0 || st->image_height <= 0)
+        return false;
+    const uint32_t gx = (uint32_t)((st->image_width + GSR_TILE_X - 1) / GSR_TILE_X);
+    const uint32_t gy = (uint32_t)((st->image_height + GSR_TILE_Y - 1) / GSR_TILE_Y);
+    uint32_t rb = 0, re = gy;
+    if (st->tile_row_begin != 0 || st->tile_row_end != 0) {
+        if (st->tile_row_begin < 0 || st->tile_row_end > (int)gy ||
+            st->tile_row_begin >= st->tile_row_end)
+            return false;  // forward_impl reports it
+        rb = (uint32_t)st->tile_row_begin;
+        re = (uint32_t)st->tile_row_end;
+    }
+    const uint32_t rows = re - rb;
+    const bool aux_ranges = ctx->fused_binning && ctx->aux_ranges &&
+                            gsr_tile_diff_cells(gx, rows) <= kTileDiffMaxCells;
+    const int col_shift = 32 - (rows > 1 ? bits_for(rows - 1) : 0);
+    return aux_ranges && ctx->column_pairs && gx <= 256 && rows <= 256 &&
+           (col_shift == 32 || (uint64_t)g->P <= (1ull << col_shift));
+}
+
+// Everything a recorded frame bakes in besides the camera and bg (staged per frame).
+std::vector<uint64_t> frame_key(const gsr_context *ctx, const gsr_gaussians *g,
+                                const gsr_raster_settings *st, const gsr_outputs *out) {
+    std::vector<uint64_t> k;
+    k.reserve(48);
+    auto u = [&](uint64_t v) { k.push_back(v); };
+    auto p = [&](const void *v) { k.push_back((uint64_t)reinterpret_cast<uintptr_t>(v)); };
+    auto f = [&](float x) {
+        uint32_t b;
+        std::memcpy(&b, &x, 4);
+        k.push_back(b);
+    };
+    u((uint64_t)g->P), u((uint64_t)g->D), u((uint64_t)g->M), f(g->scale_modifier);
+    p(g->means3D), p(g->scales), p(g->rotations), p(g->opacities), p(g->shs);
+    p(g->colors_precomp), p(g->cov3D_precomp);
+    u((uint64_t)st->image_width), u((uint64_t)st->image_height), f(st->tanfovx), f(st->tanfovy);
+    u(st->campos != nullptr), u((uint64_t)st->tile_row_begin), u((uint64_t)st->tile_row_end);
+    u((uint64_t)st->prefiltered);
+    p(out->color), p(out->radii), p(out->depths), p(out->means2D), p(out->conic_opacity);
+    p(out->rgb), p(out->tiles_touched), p(out->final_T), p(out->n_contrib);
+    u((uint64_t)ctx->cull), u((uint64_t)ctx->fast), u((uint64_t)ctx->tile_sort_shape);
+    u((uint64_t)ctx->packed_pairs), u((uint64_t)(int64_t)ctx->color_blocks);
+    u((uint64_t)(int64_t)ctx->color_waves), u((uint64_t)(int64_t)ctx->compact_sort);
+    u(ctx->blend_xcd_group), u(ctx->serial_color);
+    u(ctx->buf_gen), u((uint64_t)ctx->graph_cap);
+    return k;
+}
+
+int64_t cap_for(int64_t K) {  // pair capacity of the captured frames: K + 25 %, 64k granules
+    const int64_t c = std::max<int64_t>(K + K / 4, 1 << 16);
+    return (c + 65535) & ~int64_t(65535);
+}
+
+void drop_graphs(gsr_context *ctx, hipStream_t s) {
+    if (ctx->graphs.empty()) return;
+    (void)hipStreamSynchronize(s);  // no launch of them is still pending
+    for (auto &e : ctx->graphs) (void)hipGraphExecDestroy(e.exec);
+    ctx->graphs.clear();
+}
+
+// One frame as a replayed hipGraph (recorded on first use of its key).
+int forward_graph(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings *st,
+                  gsr_outputs *out, hipStream_t s) {
+    const int64_t P = g->P;
+    const uint32_t gx = (uint32_t)((st->image_width + GSR_TILE_X - 1) / GSR_TILE_X);
+    const uint32_t gy = (uint32_t)((st->image_height + GSR_TILE_Y - 1) / GSR_TILE_Y);
+    const bool strip = st->tile_row_begin != 0 || st->tile_row_end != 0;
+    const uint32_t rb = strip ? (uint32_t)st->tile_row_begin : 0u;
+    const uint32_t re = strip ? (uint32_t)st->tile_row_end : gy;
+    const uint64_t T_strip = (uint64_t)gx * (re - rb);
+    // every buffer the recorded frame touches, at its final size, before recording
+    const uint64_t gen0 = ctx->buf_gen;
+    GSR_TRY(reserve_P(ctx, P, s));
+    GSR_TRY(grow(ctx, ctx->ranges_local, (size_t)std::max<uint64_t>(T_strip, 1) * 8, s));
+    GSR_TRY(grow(ctx, ctx->tile_diff,
+                 (size_t)kTileDiffBlocks * gsr_tile_diff_cells(gx, re - rb) * 4, s));
+    GSR_TRY(reserve_K(ctx, ctx->graph_cap, s));
+    GSR_TRY(grow(ctx, ctx->frame, kFrameWords * 4, s));
+    if (ctx->buf_gen != gen0) drop_graphs(ctx, s);  // they point at freed buffers
+    const std::vector<uint64_t> key = frame_key(ctx, g, st, out);
+    gsr_context::Graph *hit = nullptr;
+    for (auto &e : ctx->graphs)
+        if (e.key == key) hit = &e;
+    if (!hit) {
+        if (!ctx->cap_stream)
+            GSR_HIP(hipStreamCreateWithFlags(&ctx->cap_stream, hipStreamNonBlocking),
+                    "hipStreamCreate(capture)");
+        GSR_HIP(hipStreamBeginCapture(ctx->cap_stream, hipStreamCaptureModeThreadLocal),
+                "hipStreamBeginCapture");
+        ctx->capturing = true;
+        const uint64_t gen1 = ctx->buf_gen;
+        int rc = forward_impl(ctx, g, st, out, ctx->cap_stream);
+        ctx->capturing = false;
+        hipGraph_t graph = nullptr;
+        const hipError_t e = hipStreamEndCapture(ctx->cap_stream, &graph);
+        hipGraphExec_t exec = nullptr;
+        if (rc == GSR_OK && e == hipSuccess && ctx->buf_gen == gen1 && graph)
+            rc = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) == hipSuccess
+                     ? GSR_OK
+                     : GSR_E_HIP;
+        else if (rc == GSR_OK)
+            rc = GSR_E_HIP;
+        if (graph) (void)hipGraphDestroy(graph);
+        if (rc != GSR_OK) {  // not recordable here: this context renders on the stream
+            (void)hipGetLastError();
+            ctx->graph = 0;
+            return forward_impl(ctx, g, st, out, s);
+        }
+        if (ctx->graphs.size() >= kMaxGraphs) {
+            auto lru = std::min_element(ctx->graphs.begin(), ctx->graphs.end(),
+                                        [](const gsr_context::Graph &a,
+                                           const gsr_context::Graph &b) { return a.used < b.used; });
+            (void)hipStreamSynchronize(s);
+            (void)hipGraphExecDestroy(lru->exec);
+            ctx->graphs.erase(lru);
+        }
+        gsr_context::Graph ge;
+        ge.key = key;
+        ge.exec = exec;
+        ge.point_list = ctx->cap_point_list;
+        ge.tiles_local = ctx->cap_tiles_local;
+        ge.id_mask = ctx->cap_id_mask;
+        ge.packed = ctx->cap_packed;
+        ctx->graphs.push_back(std::move(ge));
+        hit = &ctx->graphs.back();
+    }
+    hit->used = ++ctx->graph_clock;
+    uint32_t tag = ++ctx->frame_tag;
+    if (tag == 0) tag = ++ctx->frame_tag;  // 0 is the pinned word's initial value
+    ctx->have_forward = false;
+    const auto tl0 = std::chrono::steady_clock::now();
+    hipLaunchKernelGGL(k_stage_frame, dim3(1), dim3(64), 0, s, st->viewmatrix, st->projmatrix,
+                       st->campos, st->bg, static_cast<float *>(ctx->frame.p), tag);
+    GSR_HIP(hipGetLastError(), "stage launch");
+    const auto tl1 = std::chrono::steady_clock::now();
+    GSR_HIP(hipGraphLaunch(hit->exec, s), "hipGraphLaunch");
+    // K (pair count) arrives in pinned memory from the graph's k_publish_K, tagged
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+        if ((uint32_t)__atomic_load_n(&ctx->h_total[5], __ATOMIC_ACQUIRE) == tag) break;
+        if ((spin & 1023u) == 1023u &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20))
+            return fail(GSR_E_HIP, "gsr_forward: the frame's pair count never arrived");
+    }
+    const uint64_t K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
+    if (ctx->graph_stats) {  // env GSR_GRAPH_STATS: host-time split of the replayed frames
+        const auto t1 = std::chrono::steady_clock::now();
+        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        ctx->gs_acc[0] += us(tl0, tl1), ctx->gs_acc[1] += us(tl1, t0), ctx->gs_acc[2] += us(t0, t1);
+        if (++ctx->gs_n % 200 == 0)
+            std::fprintf(stderr, "gsr graph: %zu graphs, per frame: stage %.1f us, launch %.1f us, "
+                                 "K wait %.1f us\n", ctx->graphs.size(), ctx->gs_acc[0] / 200,
+                         ctx->gs_acc[1] / 200, ctx->gs_acc[2] / 200),
+                ctx->gs_acc[0] = ctx->gs_acc[1] = ctx->gs_acc[2] = 0;
+    }
+    if (K > (uint64_t)UINT32_MAX - 4096)
+        return fail(GSR_E_INVALID, "gsr_forward: more than 2^32-4097 (Gaussian, tile) pairs");
+    if ((int64_t)K > ctx->graph_cap) {
+        // the device skipped the binning and the blend: grow, render this frame on the stream
+        ctx->graph_cap = cap_for((int64_t)K);
+        return forward_impl(ctx, g, st, out, s);
+    }
+    out->num_rendered = (int64_t)K;
+    ctx->last_K = (int64_t)K;
+    ctx->last_gx = gx; ctx->last_gy = gy; ctx->last_rb = rb; ctx->last_re = re;
+    ctx->last_point_list = hit->point_list;
+    ctx->last_tiles_local = hit->tiles_local;
+    ctx->last_id_mask = hit->id_mask;
+    ctx->last_packed = hit->packed && K > 0;
+    ctx->have_forward = true;
+    return GSR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings *st,
+                gsr_outputs *out, void *stream_) {
+    if (!ctx || !g || !st || !out) return fail(GSR_E_INVALID, "gsr_forward: NULL argument");
+    hipStream_t s = static_cast<hipStream_t>(stream_);
+    if (!capturable(ctx, g, st, out)) return forward_impl(ctx, g, st, out, s);
+    if (ctx->graph_cap == 0) {  // first frame: K is learnt on the stream path
+        GSR_TRY(forward_impl(ctx, g, st, out, s));
+        ctx->graph_cap = cap_for(ctx->last_K);
+        return GSR_OK;
+    }
+    return forward_graph(ctx, g, st, out, s);
 }
 
 int gsr_get_binning(gsr_context *ctx, uint32_t *point_list, uint32_t *point_tiles,

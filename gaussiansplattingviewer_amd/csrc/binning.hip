@@ -493,7 +493,8 @@ __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict_
                                                      const uint32_t *__restrict__ d_n,
                                                      const uint32_t *__restrict__ hist, int64_t nb,
                                                      const uint32_t *__restrict__ digit_total,
-                                                     int pack_shift, uint32_t *__restrict__ out) {
+                                                     int pack_shift, uint32_t *__restrict__ out,
+                                                     uint32_t cap, uint32_t *__restrict__ d_K) {
     __shared__ ColScatterSmem c;
     __shared__ union {
         RadixTileSmem<kCW, kCIt> big;
@@ -512,6 +513,14 @@ __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict_
     uint32_t tot;
     // global start of column d for this block: all earlier columns, then earlier blocks
     const uint32_t dstart = block256_exclusive_scan(digit_total[tid], c.tmp, tot);
+    // tot = K, the frame's pair count.  A captured frame (api.hip) sized the pair buffers for
+    // `cap` before K was known: d_K = {K, 0} for the tile sort and the blend, or {0, 1} and no
+    // stores when K exceeds it (the host then grows the buffers and renders the frame again)
+    if (d_K && blockIdx.x == 0 && tid == 0) {
+        d_K[0] = tot <= cap ? tot : 0u;
+        d_K[1] = tot <= cap ? 0u : 1u;
+    }
+    if (tot > cap) return;  // block-uniform
     c.colbase[tid] = dstart + hist[(int64_t)tid * nb + blockIdx.x];
     // thread t owns segments [seg0, seg0 + w) (one per column of its rect)
     uint32_t nseg;
@@ -855,10 +864,10 @@ hipError_t gsr_launch_col_pairs_count(const uint32_t *perm, const uint2 *strip_r
 hipError_t gsr_launch_col_pairs_scatter(const uint32_t *perm, const uint2 *rect_sorted,
                                         int64_t n_max, const uint32_t *d_n, const uint32_t *hist,
                                         const uint32_t *digit_total, int pack_shift, uint32_t *out,
-                                        hipStream_t s) {
+                                        hipStream_t s, uint32_t cap, uint32_t *d_K) {
     const int64_t nb = gsr_col_blocks(n_max);
     if (nb == 0) return hipSuccess;
     hipLaunchKernelGGL(k_col_scatter, dim3((unsigned)nb), dim3(kCG), 0, s, perm, rect_sorted, d_n,
-                       hist, nb, digit_total, pack_shift, out);
+                       hist, nb, digit_total, pack_shift, out, cap, d_K);
     return hipGetLastError();
 }

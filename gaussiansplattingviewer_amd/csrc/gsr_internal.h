@@ -217,7 +217,8 @@ struct GsrPreprocessArgs {
     // per k_count_pairs block (1024): its (Gaussian, strip tile) pair count, then 1024 uint2 of
     // the OR / AND of its kept depth keys
     uint64_t *block_pairs;
-    unsigned long long *host_K;  // pinned host memory (device-mapped): [K, D] of this frame
+    unsigned long long *host_K;  // pinned host memory (device-mapped): [K, D, -, tag]
+    const uint32_t *frame_tag;   // device word: this frame's tag, stored to host_K[3] after K
     // optional debug outputs
     float *depths, *means2D, *conic_opacity, *rgb;
     uint32_t *tiles_touched;
@@ -250,7 +251,8 @@ int64_t gsr_radix_hist_words(int64_t n);
 hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
                                 uint32_t **vals_alt, int64_t n, int begin_bit, int end_bit,
                                 uint32_t *hist, uint32_t *digit_total, hipStream_t s,
-                                int shape = 0, int first_pass = 0, uint32_t *d_count = nullptr);
+                                int shape = 0, int first_pass = 0, uint32_t *d_count = nullptr,
+                                const uint32_t *d_n = nullptr);
 // k_rs_scan alone: per digit, exclusive scan of hist[d][0..nb) across tiles -> digit_total[d].
 hipError_t gsr_launch_digit_scan(uint32_t *hist, int64_t nb, uint32_t *digit_total,
                                  hipStream_t s);
@@ -333,7 +335,8 @@ hipError_t gsr_launch_col_pairs_count(const uint32_t *perm, const uint2 *strip_r
 hipError_t gsr_launch_col_pairs_scatter(const uint32_t *perm, const uint2 *rect_sorted,
                                         int64_t n_max, const uint32_t *d_n, const uint32_t *hist,
                                         const uint32_t *digit_total, int pack_shift, uint32_t *out,
-                                        hipStream_t s);
+                                        hipStream_t s, uint32_t cap = 0xFFFFFFFFu,
+                                        uint32_t *d_K = nullptr);
 hipError_t gsr_launch_digit_scan_n(uint32_t *hist, int64_t nb, uint32_t *digit_total,
                                    const uint32_t *d_n, int64_t tile, hipStream_t s);
 // Packed pair lists (gsr_launch_dup_sort_pass with pack_shift >= 0): ids = packed & mask;
@@ -377,5 +380,6 @@ struct GsrBlendArgs {
     int fast;            // 1: folded-constant FMA arithmetic + raw v_exp_f32; 0: upstream order
     uint32_t xcd_group;  // work items per XCD round-robin group (0: plain block order)
     uint32_t id_mask;    // point_list word -> Gaussian id (packed pair lists; else ~0u)
+    const uint32_t *skip;  // captured frames: nonzero -> the pair list overflowed, draw nothing
 };
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s);

@@ -315,7 +315,8 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
 // fires -- no copy, and nothing added to the main stream.  host_K[0] = K, host_K[1] = D.
 __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__restrict__ cnt,
                                                     const uint2 *__restrict__ keybits, int64_t n,
-                                                    unsigned long long *host_K) {
+                                                    unsigned long long *host_K,
+                                                    const uint32_t *__restrict__ frame_tag) {
     __shared__ unsigned long long s_w[16];
     __shared__ uint32_t s_or[16], s_and[16];
     unsigned long long v = 0;
@@ -350,6 +351,10 @@ __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__
         const unsigned long long D = diff ? 32u - (uint32_t)__clz(diff) : 0u;
         __hip_atomic_store(host_K + 1, D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(host_K, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // a captured frame's host waits for this tag (release: K and D are visible first)
+        if (frame_tag)
+            __hip_atomic_store(host_K + 3, (unsigned long long)*frame_tag, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -546,7 +551,7 @@ hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s) {
                        reinterpret_cast<unsigned long long *>(a.block_pairs), keybits);
     hipLaunchKernelGGL(k_publish_K, dim3(1), dim3(1024), 0, s,
                        reinterpret_cast<const unsigned long long *>(a.block_pairs), keybits,
-                       (int64_t)g, a.host_K);
+                       (int64_t)g, a.host_K, a.frame_tag);
     return hipGetLastError();
 }
 

@@ -225,11 +225,12 @@ static void rts_pass(const uint32_t *k, const uint32_t *v, uint32_t *ko, uint32_
 template <int kW, int kIt>
 static void rts_sort(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt, uint32_t **vals_alt,
                      int64_t n, const GsrRadixPlan &plan, int first_pass, uint32_t *hist,
-                     uint32_t *digit_total, uint32_t *d_count, hipStream_t s) {
+                     uint32_t *digit_total, uint32_t *d_count, const uint32_t *d_n,
+                     hipStream_t s) {
     for (int p = first_pass; p < plan.n; ++p) {
         const int sh = plan.shift[p], nbits = plan.nbits[p];
-        if (!d_count) {
-            const RsCount c{n, nullptr, nullptr, nullptr};
+        if (!d_count) {  // n: grids and hist stride; d_n (if set): the live count, on the device
+            const RsCount c{n, nullptr, nullptr, d_n};
             rts_pass<kW, kIt>(*keys, *vals, *keys_alt, *vals_alt, c, c, sh, nbits, hist,
                               digit_total, s);
         } else if (p == 0) {  // drop the sentinel keys; pass 0's digit totals sum to the count
@@ -251,18 +252,18 @@ static void rts_sort(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt, uint
 hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
                                 uint32_t **vals_alt, int64_t n, int begin_bit, int end_bit,
                                 uint32_t *hist, uint32_t *digit_total, hipStream_t s, int shape,
-                                int first_pass, uint32_t *d_count) {
-    if (n <= 1 && !d_count) return hipSuccess;
+                                int first_pass, uint32_t *d_count, const uint32_t *d_n) {
+    if (n <= 1 && !d_count && !d_n) return hipSuccess;
     const GsrRadixPlan plan = gsr_radix_plan(begin_bit, end_bit);
-    if (d_count && (plan.n < 2 || first_pass != 0))
+    if (d_count && (d_n || plan.n < 2 || first_pass != 0))
         return hipErrorInvalidValue;  // the count is established by passes 0 and 1
     switch (shape) {
-        case 1: rts_sort<16, 16>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, s); break;
-        case 2: rts_sort<4, 8>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, s); break;
-        case 3: rts_sort<8, 8>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, s); break;
-        case 4: rts_sort<8, 16>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, s); break;
-        case 5: rts_sort<4, 4>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, s); break;
-        default: rts_sort<4, 16>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, s); break;
+        case 1: rts_sort<16, 16>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, d_n, s); break;
+        case 2: rts_sort<4, 8>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, d_n, s); break;
+        case 3: rts_sort<8, 8>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, d_n, s); break;
+        case 4: rts_sort<8, 16>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, d_n, s); break;
+        case 5: rts_sort<4, 4>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, d_n, s); break;
+        default: rts_sort<4, 16>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, d_n, s); break;
     }
     return hipGetLastError();
 }

@@ -227,10 +227,19 @@ const char *gsr_stage_name(int i);
  *     ordered scatter) and sorts only those; 0 = pass 0 drops the others while it sorts; auto =
  *     compact on strips (tile_row_begin/end a proper subset) of >= 4M Gaussians, where most
  *     keys are dropped and pass 0 is long.  Identical results. */
+/*   GSR_OPT_GRAPH (default 0): a forward that uses the column-first binning (the default
+ *     path) is recorded once as a hipGraph per distinct set of inputs / outputs / options and
+ *     replayed: per frame one camera-staging launch, one graph launch and a wait for the pair
+ *     count K in pinned memory, instead of ~20 launches and the event hand-offs.  The pair
+ *     buffers are sized 25 % above the last K; a frame whose K exceeds them is detected on the
+ *     device (binning and blend skipped) and rendered again on the stream after growing them.
+ *     Not used while stage timing or debug is on.  Identical results.  Off by default: the
+ *     recorded frame is one stream (ROCm launches fork / join graphs ~10x slower), which
+ *     costs more GPU time than the host time it saves. */
 enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2,
        GSR_OPT_TILE_SORT_SHAPE = 4, GSR_OPT_FUSED_BINNING = 5,
        GSR_OPT_SPLIT_COLOR = 8, GSR_OPT_PACKED_PAIRS = 9, GSR_OPT_COLUMN_PAIRS = 10,
-       GSR_OPT_COMPACT_SORT = 11 };
+       GSR_OPT_COMPACT_SORT = 11, GSR_OPT_GRAPH = 12 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
 
 #ifdef __cplusplus
