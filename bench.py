@@ -426,8 +426,7 @@ def main():
                         "tiles": T_strip},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "stage_ms_note": "HIP events at every stage boundary, separate 30-frame serial pass "
-                         "(each event adds a few us); the timed region records the blend's "
-                         "two events only",
+                         "(each event adds a few us); the timed region records no events",
         "inflight": args.inflight,
         "strip_layout": (None if balancer is None else
                          {"tile_rows": [list(t) for t in balancer.current],
@@ -445,6 +444,8 @@ def main():
                      "launch_ms_source": "serial stage pass: HIP events around the kernel on "
                                          "the forward's stream, one frame at a time; frac uses it",
                      "launch_ms_inflight": round(blend_ms_timed, 5),
+                     "launch_ms_inflight_source": "blend events of slot 0 in a separate untimed "
+                                                  "pass with frames in flight",
                      "frame_achieved_gbs": round(sum(alg.values()) / (t_max / args.steps) / 1e9, 2),
                      "valu": valu_roofline(dominant, dom_ms, args.config, default_opts)},
         "cpu_baseline": None,
