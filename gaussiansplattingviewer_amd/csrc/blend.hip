@@ -224,31 +224,13 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
         }
         // one wave: its LDS writes above complete before the reads below are served
 
-#if GSR_BLEND_PIPELINED
-        auto next2 = [&](int k) { return k + 2 < count ? k + 2 : count - 2; };
-        StagedSplat a0 = s_spl[0], a1 = s_spl[1];
-        for (int k = 0;;) {
-            int kn = next2(k);
-            const StagedSplat b0 = s_spl[kn], b1 = s_spl[kn + 1];
-            composite(a0);
-            composite(a1);
-            k += 2;
-            if (k >= count) break;
-            kn = next2(k);
-            a0 = s_spl[kn];
-            a1 = s_spl[kn + 1];
-            composite(b0);
-            composite(b1);
-            k += 2;
-            if (k >= count) break;
-        }
-#else
+        // single-buffered: a software-pipelined form (the next pair's LDS reads in flight
+        // during this pair) spilled past 64 VGPRs and was slower
         for (int k = 0; k < count; k += 2) {
             const StagedSplat a0 = s_spl[k], a1 = s_spl[k + 1];
             composite(a0);
             composite(a1);
         }
-#endif
         if (!live_any()) break;
     }
 
