@@ -212,7 +212,8 @@ int reserve_P(gsr_context *ctx, int64_t P, hipStream_t s) {
     GSR_TRY(grow(ctx, ctx->block_kept, 4 * ((n + 255) / 256), s));
     GSR_TRY(grow(ctx, ctx->partials, (size_t)std::max<int64_t>(gsr_scan_blocks(P), 1) * 4, s));
     GSR_TRY(grow_zeroed(ctx, ctx->total, 16, s));  // [K (u64), look-back error flag (u32)]
-    GSR_TRY(grow(ctx, ctx->pair_count, 1024 * 16, s));  // k_count_pairs: 1024 blocks x (8 + 8 B)
+    // per preprocess block: its pair count (8 B) and kept-key OR / AND (8 B)
+    GSR_TRY(grow(ctx, ctx->pair_count, (size_t)std::max<int64_t>((P + 255) / 256, 1) * 16, s));
     GSR_TRY(grow(ctx, ctx->hist, (size_t)std::max(gsr_radix_hist_words(P),
                                                   gsr_depth_sort_hist_words(P)) * 4, s));
     // column-first binning's per-(block, column) counts: its own buffer, since reserve_K may
@@ -635,9 +636,9 @@ static int forward_impl(gsr_context *ctx, const gsr_gaussians *g, const gsr_rast
         hipStream_t as = cap_mode ? s : ctx->aux;
         if (!cap_mode)
             GSR_HIP(hipStreamWaitEvent(ctx->aux, ctx->fork, 0), "hipStreamWaitEvent(fork)");
-        // K (the pair count) first: k_count_pairs + k_publish_K store it into pinned memory;
-        // the host waits for it only after the depth sort and the scan are enqueued, so the
-        // GPU does not idle on the host round trip
+        // K (the pair count) first: k_publish_K sums the preprocess blocks' counts into pinned
+        // memory; the host waits for it only after the depth sort and the scan are enqueued,
+        // so the GPU does not idle on the host round trip
         GSR_HIP(gsr_launch_count_pairs(pa, as), "pair count launch");
         if (!cap_mode)
             GSR_HIP(hipEventRecord(ctx->kcount_ready, as), "hipEventRecord(pair count)");

@@ -214,8 +214,8 @@ struct GsrPreprocessArgs {
     // per Gaussian: strip-clipped tile rect {x0 | width << 16, strip-local row0 | rows << 16},
     // {0, 0} when it has no pair in the strip (grid dimensions < 2^16, checked by the host)
     uint2 *strip_rect;
-    // per k_count_pairs block (1024): its (Gaussian, strip tile) pair count, then 1024 uint2 of
-    // the OR / AND of its kept depth keys
+    // per k_preprocess block (ceil(P / 256)): its (Gaussian, strip tile) pair count, then as
+    // many uint2 of the OR / AND of its kept depth keys
     uint64_t *block_pairs;
     unsigned long long *host_K;  // pinned host memory (device-mapped): [K, D, -, tag]
     const uint32_t *frame_tag;   // device word: this frame's tag, stored to host_K[3] after K
@@ -231,7 +231,8 @@ hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, bool with_color, hi
 // waves_per_simd (1..7): cap on the colour waves a CU holds at once (0 = no cap).
 hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, int waves_per_simd,
                             hipStream_t s);
-// K of the frame (sum of the strip rects' pair counts) -> *a.host_K (pinned host memory).
+// K of the frame (sum of the preprocess blocks' pair counts) and D -> a.host_K (pinned host
+// memory), after the preprocess.
 hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s);
 hipError_t gsr_launch_mark_visible(const float *means3D, int64_t P, const float *viewmatrix,
                                    uint8_t *visible, hipStream_t s);

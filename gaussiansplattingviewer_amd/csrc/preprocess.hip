@@ -191,7 +191,8 @@ __device__ __forceinline__ float3 cull_data(float A, float B, float C, float o) 
 // kColor: also evaluate the colour here (one kernel, no second stream).  Returns the number
 // of (Gaussian, strip tile) pairs of Gaussian idx.
 template <bool kColor>
-__device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, int64_t idx) {
+__device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, int64_t idx,
+                                                   uint32_t &key_out) {
     int32_t radius_out = 0;
     uint32_t strip_tiles = 0, all_tiles = 0;
     uint2 strip_rect = make_uint2(0u, 0u);
@@ -289,26 +290,46 @@ __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, i
     a.radii[idx] = radius_out;
     a.strip_rect[idx] = strip_rect;
     a.sort_keys[idx] = key;  // the depth sort's values are the indices (implicit)
+    key_out = key;
     if (a.tiles_touched) a.tiles_touched[idx] = strip_tiles;
     return strip_tiles;
 }
 
-// One thread per Gaussian.  With a.block_kept (the depth sort's compaction, strips): block b
-// also stores how many of its 256 Gaussians have pairs in the strip.
+// One thread per Gaussian.  Block b also stores its share of K (the (Gaussian, strip tile)
+// pair count) and the OR / AND of its kept depth keys (k_publish_K reduces them for the host:
+// K sizes the binning, bits(OR ^ AND) the depth sort's passes), and with a.block_kept (the
+// depth sort's compaction, strips) how many of its 256 Gaussians have pairs in the strip.
+// (A separate pass re-reading the rects and keys took 7 us at C3 and 42 us on a C4 strip.)
 template <bool kColor>
 __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool kept = idx < a.P && preprocess_one<kColor>(a, idx) != 0u;
-    if (a.block_kept) {
-        __shared__ uint32_t s_cnt[4];
-        const uint32_t c = (uint32_t)__popcll(__ballot(kept));
-        if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = c;
-        __syncthreads();
-        if (threadIdx.x == 0) a.block_kept[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    uint32_t key = 0xFFFFFFFFu;
+    const uint32_t pairs = idx < a.P ? preprocess_one<kColor>(a, idx, key) : 0u;
+    const bool kept = pairs != 0u;  // has pairs in the strip <=> its depth key is kept
+    uint32_t v = pairs, o = kept ? key : 0u, an = kept ? key : 0xFFFFFFFFu;  // v <= 256 x 2^16
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        v += __shfl_xor(v, off);
+        o |= __shfl_xor(o, off);
+        an &= __shfl_xor(an, off);
+    }
+    __shared__ uint32_t s_red[4][4];
+    const uint32_t c = a.block_kept ? (uint32_t)__popcll(__ballot(kept)) : 0u;
+    if ((threadIdx.x & 63) == 0) {
+        const int w = threadIdx.x >> 6;
+        s_red[0][w] = v, s_red[1][w] = o, s_red[2][w] = an, s_red[3][w] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a.block_pairs[blockIdx.x] = (uint64_t)s_red[0][0] + s_red[0][1] + s_red[0][2] + s_red[0][3];
+        reinterpret_cast<uint2 *>(a.block_pairs + gridDim.x)[blockIdx.x] =
+            make_uint2(s_red[1][0] | s_red[1][1] | s_red[1][2] | s_red[1][3],
+                       s_red[2][0] & s_red[2][1] & s_red[2][2] & s_red[2][3]);
+        if (a.block_kept) a.block_kept[blockIdx.x] = s_red[3][0] + s_red[3][1] + s_red[3][2] + s_red[3][3];
     }
 }
 
-// One block, after k_count_pairs on the second stream (the kernel boundary makes its stores
+// One block, on the second stream after the preprocess (the kernel boundary makes its stores
 // visible): K = sum of the per-block pair counts and D = the bits in which the kept depth keys
 // differ (bits of OR ^ AND: the depth sort's pass count), stored straight into pinned host
 // memory (system scope) so the host can read them as soon as this kernel's completion event
@@ -431,48 +452,6 @@ __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
     if (a.P < 0) s_occupancy_cap[threadIdx.x] = 0u;  // never: keeps the allocation referenced
 }
 
-// K and the depth keys' bit span for the host, on the second stream right after the
-// preprocess: per-block sums of the (Gaussian, strip tile) pair counts from the packed strip
-// rects, and the OR / AND of the depth keys of the Gaussians with pairs (the sort keys the
-// depth sort keeps), grid-stride over up to 1024 blocks (at 6M Gaussians 256 blocks left the
-// pass latency-bound: 105 us on a C4 strip).
-constexpr int kCountBlocks = 1024;
-__global__ __launch_bounds__(256) void k_count_pairs(const uint2 *__restrict__ strip_rect,
-                                                     const uint32_t *__restrict__ keys, int64_t P,
-                                                     unsigned long long *__restrict__ block_pairs,
-                                                     uint2 *__restrict__ block_keybits) {
-    unsigned long long v = 0;
-    uint32_t o = 0u, a = 0xFFFFFFFFu;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P; i += (int64_t)gridDim.x * 256) {
-        const uint2 r = strip_rect[i];
-        v += (unsigned long long)((r.x >> 16) * (r.y >> 16));
-        if (r.x != 0u) {  // has pairs in the strip <=> its depth key is kept
-            const uint32_t k = keys[i];
-            o |= k;
-            a &= k;
-        }
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        v += __shfl_xor(v, off);
-        o |= __shfl_xor(o, off);
-        a &= __shfl_xor(a, off);
-    }
-    __shared__ unsigned long long s_w[4];
-    __shared__ uint32_t s_or[4], s_and[4];
-    if ((threadIdx.x & 63) == 0) {
-        s_w[threadIdx.x >> 6] = v;
-        s_or[threadIdx.x >> 6] = o;
-        s_and[threadIdx.x >> 6] = a;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        block_pairs[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-        block_keybits[blockIdx.x] = make_uint2(s_or[0] | s_or[1] | s_or[2] | s_or[3],
-                                               s_and[0] & s_and[1] & s_and[2] & s_and[3]);
-    }
-}
-
 // GaussianRasterizer.markVisible -> upstream markVisible kernel: in_frustum only.
 __global__ __launch_bounds__(256) void k_mark_visible(const float *__restrict__ means3D,
                                                       int64_t P, const float *viewmatrix,
@@ -545,10 +524,8 @@ hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, int wave
 
 hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s) {
     if (a.P == 0) return hipSuccess;
-    const unsigned g = std::min<unsigned>(kCountBlocks, grid_for(a.P));
-    uint2 *keybits = reinterpret_cast<uint2 *>(a.block_pairs + kCountBlocks);
-    hipLaunchKernelGGL(k_count_pairs, dim3(g), dim3(256), 0, s, a.strip_rect, a.sort_keys, a.P,
-                       reinterpret_cast<unsigned long long *>(a.block_pairs), keybits);
+    const unsigned g = grid_for(a.P);  // the preprocess's blocks
+    const uint2 *keybits = reinterpret_cast<const uint2 *>(a.block_pairs + g);
     hipLaunchKernelGGL(k_publish_K, dim3(1), dim3(1024), 0, s,
                        reinterpret_cast<const unsigned long long *>(a.block_pairs), keybits,
                        (int64_t)g, a.host_K, a.frame_tag);
