@@ -56,6 +56,8 @@ struct gsr_context {
         rect_sorted, pair_count;
     DevBuf ds_a, ds_b;  // depth sort: (key, id) pairs between passes (ping-pong)
     DevBuf block_kept;  // depth sort compaction (strips): kept keys per 256-Gaussian block
+    DevBuf color_ids;   // compacted strips: the kept ids the colour pass walks (4 B x P)
+    hipEvent_t compacted = nullptr;  // the compacted ids are written (main -> second stream)
     DevBuf perm;    // the depth sort's result: Gaussian ids in depth order (kept ones)
     DevBuf ds_ctl;  // depth sort control words: kept count, key bits, per-tile key stats
     DevBuf col_hist;  // column-first binning: per-(Gaussian block, column) pair counts
@@ -312,7 +314,9 @@ int gsr_create(gsr_context **out) {
                   hipSuccess &&
               hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming | hipEventReleaseToDevice) ==
                   hipSuccess &&
-              hipEventCreateWithFlags(&ctx->kcount_ready, hipEventDisableTiming) == hipSuccess;
+              hipEventCreateWithFlags(&ctx->kcount_ready, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&ctx->compacted,
+                                      hipEventDisableTiming | hipEventReleaseToDevice) == hipSuccess;
     // timing events only time: no system-scope fence (cache writeback) when they complete
     for (auto &set : ctx->ev)
         for (auto &e : set) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableSystemFence) == hipSuccess;
@@ -338,7 +342,8 @@ void gsr_destroy(gsr_context *ctx) {
                       &ctx->ds_ctl,
                       &ctx->tile_keys,     &ctx->tile_vals,
                       &ctx->tile_keys_alt, &ctx->tile_vals_alt, &ctx->ranges_local,
-                      &ctx->tile_diff,     &ctx->col_hist,      &ctx->frame};
+                      &ctx->tile_diff,     &ctx->col_hist,      &ctx->frame,
+                      &ctx->color_ids};
     for (auto &e : ctx->graphs) (void)hipGraphExecDestroy(e.exec);
     if (ctx->cap_stream) (void)hipStreamDestroy(ctx->cap_stream);
     for (DevBuf *b : bufs)
@@ -352,6 +357,7 @@ void gsr_destroy(gsr_context *ctx) {
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
     if (ctx->join) (void)hipEventDestroy(ctx->join);
     if (ctx->kcount_ready) (void)hipEventDestroy(ctx->kcount_ready);
+    if (ctx->compacted) (void)hipEventDestroy(ctx->compacted);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->h_total) (void)hipHostFree(ctx->h_total);
     delete ctx;
@@ -588,6 +594,11 @@ static int forward_impl(gsr_context *ctx, const gsr_gaussians *g, const gsr_rast
     if (pa.conic_opacity && (reinterpret_cast<uintptr_t>(pa.conic_opacity) & 15) != 0)
         return fail(GSR_E_INVALID, "gsr_forward: conic_opacity output must be 16-B aligned");
     const bool split_color = ctx->split_color;
+    // compacted strip frames: the colour pass walks the depth sort's compacted kept ids
+    // (k_color_ids) instead of every Gaussian's rect -- at a 1/8 strip of 6M Gaussians a lane
+    // in ~8 had a row to read
+    const bool color_ids = compact_sort && split_color && !cap_mode && gsr_color_ids_ok(pa);
+    if (color_ids) GSR_TRY(grow(ctx, ctx->color_ids, (size_t)P * 4, s));
     GSR_HIP(gsr_launch_preprocess(pa, !split_color, s), "preprocess launch");
     hipEvent_t *evc = ctx->ev_color[ctx->timed_frames % kTimingRing];
     struct JoinGuard {
@@ -624,9 +635,11 @@ static int forward_impl(gsr_context *ctx, const gsr_gaussians *g, const gsr_rast
     const uint32_t tag = ++ctx->sort_tag;
     auto depth_sort = [&](int p0, int p1) {
         return compact_sort
-                   ? gsr_depth_sort_compacted(pa.sort_keys, P, pa.block_kept, keys_c, ids_c, ds_a,
-                                              ds_b, perm, hist, digit_total, d_valid, p0, p1, s,
-                                              cap_mode ? nullptr : ctx->d_hostD, tag)
+                   ? gsr_depth_sort_compacted(
+                         pa.sort_keys, P, pa.block_kept, keys_c, ids_c, ds_a, ds_b, perm, hist,
+                         digit_total, d_valid, p0, p1, s, cap_mode ? nullptr : ctx->d_hostD, tag,
+                         color_ids ? static_cast<uint32_t *>(ctx->color_ids.p) : nullptr,
+                         color_ids ? ctx->compacted : nullptr)
                    : gsr_depth_sort(pa.sort_keys, P, 1, ds_a, ds_b, perm, hist, digit_total,
                                     d_valid, p0, p1, s, cap_mode ? nullptr : ctx->d_hostD, tag);
     };
@@ -643,20 +656,28 @@ static int forward_impl(gsr_context *ctx, const gsr_gaussians *g, const gsr_rast
         if (!cap_mode)
             GSR_HIP(hipEventRecord(ctx->kcount_ready, as), "hipEventRecord(pair count)");
         if (tmode == 1) GSR_HIP(hipEventRecord(evc[0], as), "hipEventRecord");
-        if (aux_ranges && ctx->aux_ranges == 1) {
+        // (with the compacted ids the ranges go first: the colour waits for the compaction)
+        const bool ranges_first = aux_ranges && (ctx->aux_ranges == 1 || color_ids);
+        if (ranges_first) {
             uint32_t *part = static_cast<uint32_t *>(ctx->tile_diff.p);
             GSR_HIP(gsr_launch_tile_ranges_aux(pa.strip_rect, P, gx, rows_tiles, part,
                                                static_cast<uint2 *>(ctx->ranges_local.p), as),
                     "tile ranges launch");
         }
         // (in a captured frame the colour runs alone: no cap)
-        GSR_HIP(gsr_launch_color(pa, ctx->color_blocks,
-                                 ctx->color_waves >= 0 ? ctx->color_waves
-                                 : cap_mode            ? 0
-                                 : P < (4 << 20)       ? 3
-                                                       : 4,
-                                 as), "color launch");
-        if (aux_ranges && ctx->aux_ranges != 1) {
+        const int color_waves = ctx->color_waves >= 0 ? ctx->color_waves
+                                : cap_mode            ? 0
+                                : P < (4 << 20)       ? 3
+                                                      : 4;
+        if (color_ids) {
+            GSR_HIP(hipStreamWaitEvent(as, ctx->compacted, 0), "hipStreamWaitEvent(compacted)");
+            GSR_HIP(gsr_launch_color_ids(pa, static_cast<const uint32_t *>(ctx->color_ids.p),
+                                         d_valid, color_waves, as),
+                    "color launch");
+        } else {
+            GSR_HIP(gsr_launch_color(pa, ctx->color_blocks, color_waves, as), "color launch");
+        }
+        if (aux_ranges && !ranges_first) {
             uint32_t *part = static_cast<uint32_t *>(ctx->tile_diff.p);
             GSR_HIP(gsr_launch_tile_ranges_aux(pa.strip_rect, P, gx, rows_tiles, part,
                                                static_cast<uint2 *>(ctx->ranges_local.p), as),

@@ -472,7 +472,8 @@ __global__ __launch_bounds__(1024) void k_ds_compact_scan(uint32_t *__restrict__
 __global__ __launch_bounds__(256) void k_ds_compact(const uint32_t *__restrict__ keys, int64_t n,
                                                     const uint32_t *__restrict__ block_off,
                                                     uint32_t *__restrict__ keys_c,
-                                                    uint32_t *__restrict__ ids_c) {
+                                                    uint32_t *__restrict__ ids_c,
+                                                    uint32_t *__restrict__ ids_copy) {
     __shared__ uint32_t s_w[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t idx = (int64_t)blockIdx.x * 256 + tid;
@@ -488,6 +489,7 @@ __global__ __launch_bounds__(256) void k_ds_compact(const uint32_t *__restrict__
         const uint32_t dst = base + (uint32_t)__popcll(bal & lt);
         keys_c[dst] = key;
         ids_c[dst] = (uint32_t)idx;
+        if (ids_copy) ids_copy[dst] = (uint32_t)idx;  // outlives ids_c (the colour pass reads it)
     }
 }
 
@@ -550,7 +552,7 @@ hipError_t gsr_depth_sort_compacted(const uint32_t *keys, int64_t n, uint32_t *b
                                     uint2 *pairs_b, uint32_t *perm, uint32_t *hist,
                                     uint32_t *digit_total, uint32_t *ctl, int pass_begin,
                                     int pass_end, hipStream_t s, unsigned long long *host_D,
-                                    uint32_t tag) {
+                                    uint32_t tag, uint32_t *ids_copy, hipEvent_t compacted) {
     if (n <= 0 || pass_begin >= pass_end) return hipSuccess;
     if (n > (int64_t)UINT32_MAX || pass_begin < 0 || pass_end > kDPasses)
         return hipErrorInvalidValue;
@@ -558,7 +560,11 @@ hipError_t gsr_depth_sort_compacted(const uint32_t *keys, int64_t n, uint32_t *b
         const int64_t nb = (n + 255) / 256;
         hipLaunchKernelGGL(k_ds_compact_scan, dim3(1), dim3(1024), 0, s, block_kept, nb, ctl);
         hipLaunchKernelGGL(k_ds_compact, dim3((unsigned)nb), dim3(256), 0, s, keys, n, block_kept,
-                           keys_c, ids_c);
+                           keys_c, ids_c, ids_copy);
+        if (compacted) {
+            const hipError_t e = hipEventRecord(compacted, s);
+            if (e != hipSuccess) return e;
+        }
     }
     // the passes read the compacted count from ctl[0] (grids sized for n)
     return ds_passes(keys_c, ids_c, ctl, n, 0, pairs_a, pairs_b, perm, hist, digit_total, ctl,

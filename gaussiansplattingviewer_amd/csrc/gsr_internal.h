@@ -231,6 +231,11 @@ hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, bool with_color, hi
 // waves_per_simd (1..7): cap on the colour waves a CU holds at once (0 = no cap).
 hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, int waves_per_simd,
                             hipStream_t s);
+// Colour of the Gaussians listed in ids[0 .. *d_n) (the depth sort's compacted kept ids of a
+// strip frame), degree-3 16-B-aligned SH and no rgb output only (gsr_color_ids_ok).
+bool gsr_color_ids_ok(const GsrPreprocessArgs &a);
+hipError_t gsr_launch_color_ids(const GsrPreprocessArgs &a, const uint32_t *ids,
+                                const uint32_t *d_n, int waves_per_simd, hipStream_t s);
 // K of the frame (sum of the preprocess blocks' pair counts) and D -> a.host_K (pinned host
 // memory), after the preprocess.
 hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s);
@@ -296,7 +301,8 @@ hipError_t gsr_depth_sort_compacted(const uint32_t *keys, int64_t n, uint32_t *b
                                     uint2 *pairs_b, uint32_t *perm, uint32_t *hist,
                                     uint32_t *digit_total, uint32_t *ctl, int pass_begin,
                                     int pass_end, hipStream_t s,
-                                    unsigned long long *host_D = nullptr, uint32_t tag = 0);
+                                    unsigned long long *host_D = nullptr, uint32_t tag = 0,
+                                    uint32_t *ids_copy = nullptr, hipEvent_t compacted = nullptr);
 
 // Binning: offsets scan over depth-sorted strip tile counts, duplicate into (tile, id)
 // pairs, and tile ranges.

@@ -452,6 +452,25 @@ __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
     if (a.P < 0) s_occupancy_cap[threadIdx.x] = 0u;  // never: keeps the allocation referenced
 }
 
+// The colour pass of a compacted strip frame: one lane per kept Gaussian of ids[0 .. *d_n)
+// (k_ds_compact's list), so every lane of a wave reads a row instead of ~1 in 8 on a 1/8 strip,
+// and the P-long rect scan is gone.  Same row streaming and occupancy cap as k_color.
+__global__ __launch_bounds__(256) void k_color_ids(const GsrPreprocessArgs a,
+                                                   const uint32_t *__restrict__ ids,
+                                                   const uint32_t *__restrict__ d_n) {
+    extern __shared__ uint32_t s_occupancy_cap[];
+    const int64_t n = *d_n;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const int64_t idx = ids[i];
+        const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1],
+                                     a.means3D[3 * idx + 2]);
+        store_color(a, idx, eval_sh3_stream(p, a.campos,
+                                            reinterpret_cast<const float4 *>(a.shs) + idx * 12));
+    }
+    if (a.P < 0) s_occupancy_cap[threadIdx.x] = 0u;  // never: keeps the allocation referenced
+}
+
 // GaussianRasterizer.markVisible -> upstream markVisible kernel: in_frustum only.
 __global__ __launch_bounds__(256) void k_mark_visible(const float *__restrict__ means3D,
                                                       int64_t P, const float *viewmatrix,
@@ -519,6 +538,21 @@ hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, int wave
         }
     }
     hipLaunchKernelGGL(k_color, dim3(g), dim3(256), lds, s, a);
+    return hipGetLastError();
+}
+
+bool gsr_color_ids_ok(const GsrPreprocessArgs &a) {
+    return a.sh_vec4 && !a.colors_precomp && a.D == 3 && !a.rgb;
+}
+
+hipError_t gsr_launch_color_ids(const GsrPreprocessArgs &a, const uint32_t *ids,
+                                const uint32_t *d_n, int waves_per_simd, hipStream_t s) {
+    if (a.P == 0) return hipSuccess;
+    if (!gsr_color_ids_ok(a)) return hipErrorInvalidValue;
+    size_t lds = 0;
+    if (waves_per_simd >= 3 && waves_per_simd < 8)
+        lds = (size_t)(160 * 1024 / waves_per_simd) & ~(size_t)1023;
+    hipLaunchKernelGGL(k_color_ids, dim3(grid_for(a.P)), dim3(256), lds, s, a, ids, d_n);
     return hipGetLastError();
 }
 
