@@ -141,11 +141,13 @@ __global__ __launch_bounds__(kDThreads) void k_ds_upsweep(const void *__restrict
 }
 
 // Block b: digits [16 b, 16 b + 16); thread t: digit 16 b + t % 16 over tile group t / 16 (a
-// sixteenth of the tiles, loaded kScanReg at a time so the loads are in flight together).
+// sixteenth of the tiles, loaded kScanReg at a time so the loads are in flight together; up to
+// kScanReg tiles per thread -- 256 tiles, 1M keys -- stay in registers for the write-back
+// instead of being loaded again).
 // hist[t][d] becomes the exclusive count of digit d in tiles < t; digit_total[d] the count
 // over all tiles.  Pass 0: the last block also reduces the tiles' {OR, AND, kept} into ctl[0]
 // (kept) and ctl[1] (D).
-constexpr int kScanDigits = 16, kScanGroups = 16, kScanReg = 8;
+constexpr int kScanDigits = 16, kScanGroups = 16, kScanReg = 16;
 template <bool kFirst>
 __global__ __launch_bounds__(256) void k_ds_scan(uint32_t *__restrict__ hist, int64_t n_host,
                                                  uint32_t *__restrict__ ctl, int shift,
@@ -169,6 +171,7 @@ __global__ __launch_bounds__(256) void k_ds_scan(uint32_t *__restrict__ hist, in
         const uint32_t t1 = (uint32_t)((uint64_t)nt * (g + 1) / kScanGroups);
         uint32_t *col = hist + d;
         uint32_t v[kScanReg], s = 0;
+        const bool kept = t1 - t0 <= (uint32_t)kScanReg;  // one load round, values kept
         for (uint32_t t = t0; t < t1; t += kScanReg) {
 #pragma unroll
             for (int r = 0; r < kScanReg; ++r)
@@ -186,9 +189,11 @@ __global__ __launch_bounds__(256) void k_ds_scan(uint32_t *__restrict__ hist, in
             tot += x;
         }
         for (uint32_t t = t0; t < t1; t += kScanReg) {
+            if (!kept) {
 #pragma unroll
-            for (int r = 0; r < kScanReg; ++r)
-                v[r] = t + r < t1 ? col[(int64_t)(t + r) * kDBins] : 0u;
+                for (int r = 0; r < kScanReg; ++r)
+                    v[r] = t + r < t1 ? col[(int64_t)(t + r) * kDBins] : 0u;
+            }
 #pragma unroll
             for (int r = 0; r < kScanReg; ++r) {
                 if (t + r < t1) col[(int64_t)(t + r) * kDBins] = pre;
