@@ -39,7 +39,10 @@ def test_sort_backend_contract(gpu, golden):
     np.testing.assert_array_equal(d[out[:, 0]], d[ref[:, 0]])
 
 
-@pytest.mark.parametrize("P", [1, 2, 4095, 4097, 8191, 8192, 8193, 40_000, 1_000_000, 6_000_000])
+# 1,048,576 / 1,048,577: 256 / 257 sort tiles, where the digit scan's threads stop keeping their
+# 16 tile counts in registers and load them again for the write-back (depth_sort.hip k_ds_scan)
+@pytest.mark.parametrize("P", [1, 2, 4095, 4097, 8191, 8192, 8193, 40_000, 1_000_000, 1_048_576,
+                               1_048_577, 6_000_000])
 def test_stable_permutation_full_size(gpu, P):
     rng = np.random.default_rng(P)
     xyz = rng.standard_normal((P, 3)).astype(np.float32)
@@ -53,7 +56,7 @@ def test_stable_permutation_full_size(gpu, P):
     assert np.all(ds[1:] >= ds[:-1])                           # ascending
     tie = ds[1:] == ds[:-1]
     assert np.all(idx[1:][tie] > idx[:-1][tie])                # stable among ties
-    if P <= 1_000_000:
+    if P <= 1_048_577:
         np.testing.assert_array_equal(idx, np.argsort(depth, kind="stable"))
 
 
