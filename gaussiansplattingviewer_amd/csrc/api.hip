@@ -84,10 +84,12 @@ struct gsr_context {
     int fast = 1;
     int tile_sort_shape = 3;  // 8 waves x 8 keys/lane: fastest measured
     int fused_binning = 1;    // duplicate fused with the first tile-sort pass
-    // tile ranges from the rects' per-tile counts on the second stream, after the colour
-    // (2; 1 = before it: the colour then overlaps the duplicate stage instead of the depth
-    // sort and the frame is ~2% slower; 0 = k_ranges on the main stream).  env GSR_AUX_RANGES
-    int aux_ranges = 2;
+    // tile ranges from the rects' per-tile counts on the second stream, before the colour (1;
+    // the colour then overlaps the column count and scatter rather than the depth sort: C3 with
+    // two frames in flight 3,470 -> 3,600 fps, serial +0.5 %, C2 +9 %, C4 and its strips even;
+    // 2 = after the colour, the round-2 default; 0 = k_ranges on the main stream).  env
+    // GSR_AUX_RANGES
+    int aux_ranges = 1;
     // GSR_OPT_PACKED_PAIRS: one 32-bit word per (tile, Gaussian) pair -- the tile-id bits the
     // second tile-sort pass needs above the Gaussian id -- instead of a key and a value array
     // (needs the second-stream ranges; falls back when the bits do not fit)
