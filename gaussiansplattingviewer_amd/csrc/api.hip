@@ -270,7 +270,7 @@ int gsr_create(gsr_context **out) {
         delete ctx;
         return fail(GSR_E_HIP, "gsr_create: no HIP device");
     }
-    if (hipHostMalloc(reinterpret_cast<void **>(&ctx->h_total), 6 * sizeof(uint64_t),
+    if (hipHostMalloc(reinterpret_cast<void **>(&ctx->h_total), 8 * sizeof(uint64_t),
                       hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->d_hostK), ctx->h_total + 2, 0) !=
             hipSuccess ||
@@ -280,7 +280,7 @@ int gsr_create(gsr_context **out) {
         delete ctx;
         return fail(GSR_E_HIP, "gsr_create: hipHostMalloc failed");
     }
-    std::memset(ctx->h_total, 0, 6 * sizeof(uint64_t));  // tag 0 never matches a frame
+    std::memset(ctx->h_total, 0, 8 * sizeof(uint64_t));  // tag 0 never matches a frame
     int prio_least = 0, prio_greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) {
         (void)hipGetLastError();
@@ -654,6 +654,7 @@ static int forward_impl(gsr_context *ctx, const gsr_gaussians *g, const gsr_rast
         // K (the pair count) first: k_publish_K sums the preprocess blocks' counts into pinned
         // memory; the host waits for it only after the depth sort and the scan are enqueued,
         // so the GPU does not idle on the host round trip
+        pa.k_tag = cap_mode ? 0u : (tag ? tag : 1u);  // (launched after the preprocess)
         GSR_HIP(gsr_launch_count_pairs(pa, as), "pair count launch");
         if (!cap_mode)
             GSR_HIP(hipEventRecord(ctx->kcount_ready, as), "hipEventRecord(pair count)");
@@ -752,7 +753,22 @@ static int forward_impl(gsr_context *ctx, const gsr_gaussians *g, const gsr_rast
         K = (uint64_t)ctx->graph_cap;  // an upper bound; the device knows the real K
         if (!colpairs) return fail(GSR_E_STATE, "gsr_forward: frame not capturable");
     } else if (split_color) {
-        GSR_HIP(hipEventSynchronize(ctx->kcount_ready), "hipEventSynchronize(pair count)");
+        // spin on the frame's K tag (pinned memory, written by k_publish_K after K): a sleeping
+        // event wait adds wake-up jitter to every frame; the event stays the fallback
+        const uint64_t want = pa.k_tag;
+        const auto t0 = std::chrono::steady_clock::now();
+        bool got = false;
+        for (uint32_t spin = 0;; ++spin) {
+            if (__atomic_load_n(&ctx->h_total[7], __ATOMIC_ACQUIRE) == want) {
+                got = true;
+                break;
+            }
+            if ((spin & 1023u) == 1023u &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
+                break;
+        }
+        if (!got)
+            GSR_HIP(hipEventSynchronize(ctx->kcount_ready), "hipEventSynchronize(pair count)");
         K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
         if (dbg) {  // the pair count's D and the sort's own D (pass 0) agree
             uint32_t ctl2[2];

@@ -217,8 +217,9 @@ struct GsrPreprocessArgs {
     // per k_preprocess block (ceil(P / 256)): its (Gaussian, strip tile) pair count, then as
     // many uint2 of the OR / AND of its kept depth keys
     uint64_t *block_pairs;
-    unsigned long long *host_K;  // pinned host memory (device-mapped): [K, D, -, tag]
+    unsigned long long *host_K;  // pinned host memory (device-mapped): [K, D, -, tag, -, ktag]
     const uint32_t *frame_tag;   // device word: this frame's tag, stored to host_K[3] after K
+    uint32_t k_tag;              // else (nonzero): stored to host_K[5] after K (the host spins)
     // optional debug outputs
     float *depths, *means2D, *conic_opacity, *rgb;
     uint32_t *tiles_touched;

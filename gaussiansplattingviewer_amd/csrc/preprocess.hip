@@ -337,7 +337,8 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
 __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__restrict__ cnt,
                                                     const uint2 *__restrict__ keybits, int64_t n,
                                                     unsigned long long *host_K,
-                                                    const uint32_t *__restrict__ frame_tag) {
+                                                    const uint32_t *__restrict__ frame_tag,
+                                                    uint32_t k_tag) {
     __shared__ unsigned long long s_w[16];
     __shared__ uint32_t s_or[16], s_and[16];
     unsigned long long v = 0;
@@ -375,6 +376,10 @@ __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__
         // a captured frame's host waits for this tag (release: K and D are visible first)
         if (frame_tag)
             __hip_atomic_store(host_K + 3, (unsigned long long)*frame_tag, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        // a stream frame's host spins on this tag instead of sleeping in an event wait
+        else if (k_tag)
+            __hip_atomic_store(host_K + 5, (unsigned long long)k_tag, __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -562,7 +567,7 @@ hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s) {
     const uint2 *keybits = reinterpret_cast<const uint2 *>(a.block_pairs + g);
     hipLaunchKernelGGL(k_publish_K, dim3(1), dim3(1024), 0, s,
                        reinterpret_cast<const unsigned long long *>(a.block_pairs), keybits,
-                       (int64_t)g, a.host_K, a.frame_tag);
+                       (int64_t)g, a.host_K, a.frame_tag, a.k_tag);
     return hipGetLastError();
 }
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Interleaved sweep of tuning knobs on one box (C3 by default, BENCH_ARGS to change): each
-# entry of KNOBS is "ENV=.. [--bench-flag]"; "-" is the default.  Prints fps, serial ms and
+# entry of KNOBS is "ENV=.. [--bench-flag[=value]]"; "-" is the default.  Prints fps, serial ms and
 # stage times per run.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
