@@ -71,7 +71,6 @@ struct gsr_context {
     unsigned long long *d_hostK = nullptr;  // device view of h_total + 2
     unsigned long long *d_hostD = nullptr;  // device view of h_total + 4
     uint32_t sort_tag = 0;                  // frames sorted on this context (tags h_total[4])
-    hipEvent_t kcount_ready = nullptr;  // the pair counts of this frame are on the host
     // state of the last forward (for gsr_get_binning)
     bool have_forward = false;
     int64_t last_K = 0;
@@ -316,7 +315,6 @@ int gsr_create(gsr_context **out) {
                   hipSuccess &&
               hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming | hipEventReleaseToDevice) ==
                   hipSuccess &&
-              hipEventCreateWithFlags(&ctx->kcount_ready, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&ctx->compacted,
                                       hipEventDisableTiming | hipEventReleaseToDevice) == hipSuccess;
     // timing events only time: no system-scope fence (cache writeback) when they complete
@@ -358,7 +356,6 @@ void gsr_destroy(gsr_context *ctx) {
             if (e) (void)hipEventDestroy(e);
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
     if (ctx->join) (void)hipEventDestroy(ctx->join);
-    if (ctx->kcount_ready) (void)hipEventDestroy(ctx->kcount_ready);
     if (ctx->compacted) (void)hipEventDestroy(ctx->compacted);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->h_total) (void)hipHostFree(ctx->h_total);
@@ -656,8 +653,6 @@ static int forward_impl(gsr_context *ctx, const gsr_gaussians *g, const gsr_rast
         // so the GPU does not idle on the host round trip
         pa.k_tag = cap_mode ? 0u : (tag ? tag : 1u);  // (launched after the preprocess)
         GSR_HIP(gsr_launch_count_pairs(pa, as), "pair count launch");
-        if (!cap_mode)
-            GSR_HIP(hipEventRecord(ctx->kcount_ready, as), "hipEventRecord(pair count)");
         if (tmode == 1) GSR_HIP(hipEventRecord(evc[0], as), "hipEventRecord");
         // (with the compacted ids the ranges go first: the colour waits for the compaction)
         const bool ranges_first = aux_ranges && (ctx->aux_ranges == 1 || color_ids);
@@ -754,7 +749,8 @@ static int forward_impl(gsr_context *ctx, const gsr_gaussians *g, const gsr_rast
         if (!colpairs) return fail(GSR_E_STATE, "gsr_forward: frame not capturable");
     } else if (split_color) {
         // spin on the frame's K tag (pinned memory, written by k_publish_K after K): a sleeping
-        // event wait adds wake-up jitter to every frame; the event stays the fallback
+        // event wait adds wake-up jitter to every frame (and its record a host call); after
+        // 50 ms without the tag, wait for the second stream instead (it reports a fault)
         const uint64_t want = pa.k_tag;
         const auto t0 = std::chrono::steady_clock::now();
         bool got = false;
@@ -767,8 +763,7 @@ static int forward_impl(gsr_context *ctx, const gsr_gaussians *g, const gsr_rast
                 std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
                 break;
         }
-        if (!got)
-            GSR_HIP(hipEventSynchronize(ctx->kcount_ready), "hipEventSynchronize(pair count)");
+        if (!got) GSR_HIP(hipStreamSynchronize(ctx->aux), "hipStreamSynchronize(pair count)");
         K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
         if (dbg) {  // the pair count's D and the sort's own D (pass 0) agree
             uint32_t ctl2[2];
