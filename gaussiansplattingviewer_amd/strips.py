@@ -85,6 +85,7 @@ class StripBalancer:
         self.current = strip_layout(grid_y, world)
         self.pending = None  # (apply_at, work, vec, host, event)
         self.history = []    # (frame, layout) of every change (diagnostics)
+        self._side = None    # the one stream the counts' device -> host copies run on
 
     def layout(self, frame: int) -> list[tuple[int, int]]:
         p = self.pending
@@ -114,7 +115,11 @@ class StripBalancer:
         vec[b:e].copy_(row_pairs)
         work = dist.all_reduce(vec, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         if vec.is_cuda:
-            side = torch.cuda.Stream(device=vec.device)
+            # one side stream for the run (a new stream per observation would take another of
+            # torch's pooled streams each time, spreading work over more hardware queues)
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=vec.device)
+            side = self._side
             host = torch.empty((self.gy,), dtype=torch.int32, pin_memory=True)
             with torch.cuda.stream(side):
                 work.wait()  # the side stream waits for the all-reduce
