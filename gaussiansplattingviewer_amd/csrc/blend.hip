@@ -100,6 +100,7 @@ struct StagedSplat {
 template <bool kFast, bool kContrib>
 __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_t n_work) {
     __shared__ StagedSplat s_spl[64];
+    constexpr bool kPair = kFast && !kContrib;  // paired colour / bound words (see staging)
 
     const uint32_t b = blockIdx.x;
     const uint32_t work = xcd_work(b, a.xcd_group);
@@ -209,7 +210,17 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
             }
             const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
             const int slot = __popcll(bal & lt);  // compacted in list order
-            s_spl[slot] = st;
+            if (kPair) {
+                // a pair's blues and power bounds share the even slot's e: {b0, b1, bound0,
+                // bound1} (5 LDS reads per composited pair instead of 6)
+                s_spl[slot].g = st.g;
+                s_spl[slot].q = st.q;
+                float *pe = &s_spl[slot & ~1].e.x;
+                pe[slot & 1] = st.e.x;
+                pe[2 + (slot & 1)] = st.e.z;
+            } else {
+                s_spl[slot] = st;
+            }
         }
         int count = __popcll(bal);
         if (count == 0) continue;
@@ -217,9 +228,14 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
         // an opacity-0 splat in slot `count` (< 64 for an odd count): exact: opacity 0; fast:
         // exponent 0 against a power bound of -inf (never visible)
         if (count & 1) {
-            if (lane < 12)
+            if (kPair) {
+                if (lane < 8) reinterpret_cast<float *>(&s_spl[count])[lane] = 0.0f;
+                if (lane == 8) s_spl[count - 1].e.y = 0.0f;
+                if (lane == 9) s_spl[count - 1].e.w = -__builtin_huge_valf();
+            } else if (lane < 12) {
                 reinterpret_cast<float *>(&s_spl[count])[lane] =
                     (kFast && lane == 10) ? -__builtin_huge_valf() : 0.0f;
+            }
             ++count;
         }
         // one wave: its LDS writes above complete before the reads below are served
@@ -227,9 +243,16 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
         // single-buffered: a software-pipelined form (the next pair's LDS reads in flight
         // during this pair) spilled past 64 VGPRs and was slower
         for (int k = 0; k < count; k += 2) {
-            const StagedSplat a0 = s_spl[k], a1 = s_spl[k + 1];
-            composite(a0);
-            composite(a1);
+            if (kPair) {
+                const float4 e = s_spl[k].e;
+                composite(StagedSplat{s_spl[k].g, s_spl[k].q, make_float4(e.x, 0.0f, e.z, 0.0f)});
+                composite(
+                    StagedSplat{s_spl[k + 1].g, s_spl[k + 1].q, make_float4(e.y, 0.0f, e.w, 0.0f)});
+            } else {
+                const StagedSplat a0 = s_spl[k], a1 = s_spl[k + 1];
+                composite(a0);
+                composite(a1);
+            }
         }
         if (!live_any()) break;
     }
