@@ -75,7 +75,8 @@ __device__ __forceinline__ uint32_t xcd_work(uint32_t b, uint32_t group) {
     return ((l / group) * 8u + x) * group + l % group;
 }
 
-// One staged splat as the inner loop reads it: three 16-B LDS reads from one address.
+// One staged splat as the inner loop reads it: three 16-B LDS reads from one address (fast
+// arithmetic without n_contrib: a pair shares the even slot's e = {b0, b1, bound0, bound1}).
 // exact: g = x, y, conic a, conic b; q = conic c, opacity, r, g; e = b, position + 1 (uint bits:
 // upstream's `contributor`), -, -.
 // fast: the exponent as a quadratic in the lane's offset (u, v) from the quadrant centre,
