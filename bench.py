@@ -113,7 +113,7 @@ class Scene:
 # tools/profile.sh + tools/prof_summary.py --json) of the default configuration, and the kernel
 # each stage's roofline refers to.  The bench cannot read PMC counters itself; the profile is
 # of this same command (c3, default options).
-TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r02f_c3_kernels.json")
+TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r02g_c3_kernels.json")
 STAGE_KERNEL = {"blend": "k_blend_q<true, false>", "preprocess": "k_preprocess<false>",
                 "color": "k_color", "depth_sort": None, "duplicate": "k_col_scatter",
                 "tile_sort": None, "scan": None, "ranges": None}
@@ -139,7 +139,7 @@ def measured_traffic(stage, config, default_opts):
 # busy = SQ_INSTS_VALU x 2 cycles (a wave64 VALU instruction issues over 2 cycles) / (1024
 # SIMDs x kernel cycles).  SQ_INSTS_VALU is exact: it reads the known instruction count of a
 # calibration kernel (tools/micro/valu_calib.hip, profiles/r02_valu_calibration.md).
-VALU_PROFILE = os.path.join(REPO, "profiles", "r02f_c3_blend_sq.json")
+VALU_PROFILE = os.path.join(REPO, "profiles", "r02g_c3_blend_sq.json")
 VALU_PEAK_T = 256 * 4 * 32 * 2.4e9 / 1e12
 
 
