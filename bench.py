@@ -12,11 +12,12 @@ launched by torch.distributed.run) the frame's 16-px tile rows are split into N 
 rank renders its strip and rank 0 gathers the frame over RCCL (strong scaling: the frame is
 fixed, N grows).
 
-Prints ONE JSON line on rank 0.  `roofline` is for the dominant kernel (the blend): its
-algorithmic bytes over its launch duration from HIP events of a serial pass, with measured HBM
-traffic and a VALU roof from committed rocprofv3 PMC profiles; `cpu_baseline` times, on rank 0
-at N = 1, the reference's own CPU sort path (renderer_ogl.py:10-19, restated and pinned in
-oracle/) and the CPU oracle of the whole forward (oracle/, a C port, 1 thread).
+Prints ONE JSON line on rank 0.  `roofline` is for the dominant kernel (the blend) on the roof
+that bounds it, VALU: its instructions per launch (a committed rocprofv3 SQ profile of this
+build) over its launch duration from HIP events of a serial pass, with the HBM roof from the
+committed FETCH/WRITE counters beside it; `cpu_baseline` times, on rank 0 at N = 1, the
+reference's own CPU sort path (renderer_ogl.py:10-19, restated and pinned in oracle/) and the
+CPU oracle of the whole forward (oracle/, a C port, OpenMP over the host cores).
 """
 from __future__ import annotations
 
@@ -37,7 +38,7 @@ sys.path.insert(0, REPO)
 
 from gaussiansplattingviewer_amd import _lib  # noqa: E402
 from gaussiansplattingviewer_amd.camera import cuda_camera_inputs, orbit_eye, static_camera  # noqa: E402
-from gaussiansplattingviewer_amd.gaussian_data import synthetic_gaussians  # noqa: E402
+from gaussiansplattingviewer_amd.gaussian_data import clustered_scene, synthetic_gaussians  # noqa: E402
 from gaussiansplattingviewer_amd.rasterizer import rasterize_gaussians_native, tile_row_pairs  # noqa: E402
 from gaussiansplattingviewer_amd.pipeline import FramePipeline  # noqa: E402
 from gaussiansplattingviewer_amd.strips import (StripBalancer, StripGather, strip_pixel_rows,  # noqa: E402
@@ -46,11 +47,14 @@ from gaussiansplattingviewer_amd.strips import (StripBalancer, StripGather, stri
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 
 CONFIGS = {
-    # name: (P, W, H, sh_degree, seed, camera)
+    # name: (P, W, H, sh_degree, seed, camera[, scene generator])
     "c2": (100_000, 1920, 1080, 0, 1, "static"),
     "c3": (1_000_000, 1920, 1080, 3, 2, "static"),
     "c4": (6_000_000, 3840, 2160, 3, 3, "static"),
     "c5": (1_000_000, 1920, 1080, 3, 2, "orbit"),
+    # C3 with a capture-like scene (gaussian_data.clustered_scene): clustered centres, ground
+    # plane, background shell, near floaters; depths over 8 float exponents
+    "c3r": (1_000_000, 1920, 1080, 3, 7, "static", "clustered"),
 }
 METRIC = "frames/sec + Msplats/sec, 1M Gaussians @ 1920×1080, 1/2/4/8 MI355X"
 
@@ -62,13 +66,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--sort-shape", type=int, default=None, help="GSR_OPT_TILE_SORT_SHAPE (tuning)")
-    ap.add_argument("--unfused", action="store_true", help="GSR_OPT_FUSED_BINNING=0 (tuning)")
     ap.add_argument("--sim-strip", default=None, metavar="R/N",
                     help="diagnostic, 1 GPU: render only strip R of an N-way partition (no "
                          "gather) to estimate one rank's share of an N-GPU frame")
-    ap.add_argument("--inline-color", action="store_true",
-                    help="GSR_OPT_SPLIT_COLOR=0: colour inside the preprocess kernel (tuning)")
     ap.add_argument("--blend", default="fast", choices=["exact", "fast"],
                     help="blend arithmetic: GSR_OPT_BLEND_FAST (default) or upstream's exact "
                          "operation order")
@@ -76,15 +76,17 @@ def parse():
                     help="frames in flight (FramePipeline: own stream + context slot each); "
                          "1 = serial forwards")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
-                    help="minimum CPU-oracle time to sample for cpu_baseline")
+                    help="CPU-oracle time to sample for cpu_baseline (whole frames; at least one)")
     return ap.parse_args()
 
 
 class Scene:
     def __init__(self, cfg, dev):
-        P, W, H, deg, seed, cam_kind = CONFIGS[cfg]
+        P, W, H, deg, seed, cam_kind = CONFIGS[cfg][:6]
         self.P, self.W, self.H, self.deg, self.cam_kind = P, W, H, deg, cam_kind
-        g = synthetic_gaussians(P, deg, seed)
+        self.generator = CONFIGS[cfg][6] if len(CONFIGS[cfg]) > 6 else "uniform"
+        g = (clustered_scene(P, seed) if self.generator == "clustered"
+             else synthetic_gaussians(P, deg, seed))
         self.host = g
         up = lambda a: torch.as_tensor(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         self.xyz, self.rot, self.scale, self.opacity = up(g.xyz), up(g.rot), up(g.scale), up(g.opacity)
@@ -109,54 +111,107 @@ class Scene:
                                           tile_rows=tile_rows, slot=slot, out_color=out_color)
 
 
-# Measured HBM traffic per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate PMC passes;
-# tools/profile.sh + tools/prof_summary.py --json) of the default configuration, and the kernel
-# each stage's roofline refers to.  The bench cannot read PMC counters itself; the profile is
-# of this same command (c3, default options).
-TRAFFIC_PROFILE = os.path.join(REPO, "profiles", "r02g_c3_kernels.json")
-STAGE_KERNEL = {"blend": "k_blend_q<true, false>", "preprocess": "k_preprocess<false>",
-                "color": "k_color", "depth_sort": None, "duplicate": "k_col_scatter",
-                "tile_sort": None, "scan": None, "ranges": None}
+# Committed rocprofv3 profiles (tools/profile_config.sh on the GPU box, summarised here by
+# tools/prof_summary.py and tools/sq_summary.py): per config, the serial kernel trace with HBM
+# traffic per launch (FETCH_SIZE x2 + WRITE_SIZE, separate PMC passes) in
+# profiles/<tag>_<config>_kernels.json, and the blend's SQ counters in
+# profiles/<tag>_<config>_blend_sq.json.  Every profile records the sha256 of the libgsr.so it
+# measured; the bench uses only a profile of the library it has loaded (instruction counts and
+# traffic belong to one build), else reports null.
+PROFILES = os.path.join(REPO, "profiles")
+VALU_PEAK_T = 256 * 4 * 32 * 2.4e9 / 1e12  # lane-instructions/s: 256 CUs x 4 SIMD32 x 2.4 GHz
+BLEND_KERNEL = "k_blend_q"
 
 
-def measured_traffic(stage, config, default_opts):
-    if config != "c3" or not default_opts or not os.path.exists(TRAFFIC_PROFILE):
-        return None, None
-    k = STAGE_KERNEL.get(stage)
-    kernels = json.load(open(TRAFFIC_PROFILE))
-    # kernel names are matched by prefix (template arguments vary between builds)
-    rec = next((v for name, v in kernels.items() if name.startswith(k)), None) if k else None
-    if not rec or rec.get("read_bytes_x2") is None or rec.get("write_bytes") is None:
-        return None, None
-    return int(rec["read_bytes_x2"] + rec["write_bytes"]), os.path.relpath(TRAFFIC_PROFILE, REPO)
+def lib_sha16() -> str:
+    import hashlib
+    return hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()[:16]
 
 
-# VALU roofline of the blend ("additionally reported against FP32 VALU
-# peak"): per-launch SQ counters of the blend kernel from a committed PMC profile of this
-# command (tools/pmc_sq.sh + tools/sq_summary.py --json).  achieved = SQ_INSTS_VALU (wave64
-# instructions) x 64 lanes / launch time; peak = 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz =
-# 78.6 T lane-instructions/s (the 157.3 TFLOP/s FP32 vector peak counts an FMA as 2 flops).
-# busy = SQ_INSTS_VALU x 2 cycles (a wave64 VALU instruction issues over 2 cycles) / (1024
-# SIMDs x kernel cycles).  SQ_INSTS_VALU is exact: it reads the known instruction count of a
-# calibration kernel (tools/micro/valu_calib.hip, profiles/r02_valu_calibration.md).
-VALU_PROFILE = os.path.join(REPO, "profiles", "r02g_c3_blend_sq.json")
-VALU_PEAK_T = 256 * 4 * 32 * 2.4e9 / 1e12
+def find_profile(config: str, suffix: str):
+    """The newest committed profile of this config whose lib_sha16 is the loaded library's."""
+    import glob
+    sha = lib_sha16()
+    best = None
+    for path in glob.glob(os.path.join(PROFILES, f"*_{config}_{suffix}.json")):
+        try:
+            prof = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if prof.get("lib_sha16") == sha and (best is None or path > best[0]):
+            best = (path, prof)
+    return best
 
 
-def valu_roofline(stage, launch_ms, config, default_opts):
-    if stage != "blend" or config != "c3" or not default_opts or not os.path.exists(VALU_PROFILE):
+def measured_traffic(config: str, kernel: str):
+    """HBM bytes per launch of `kernel` from the config's committed PMC profile (FETCH_SIZE
+    doubled per the gfx950 calibration, MI355X_MICROARCH.md §HBM, + WRITE_SIZE), with the
+    profile's own average launch time; None without a profile of this build."""
+    hit = find_profile(config, "kernels")
+    if not hit:
         return None
-    prof = json.load(open(VALU_PROFILE))
-    c = prof["per_launch"]
-    lane_instr = c["SQ_INSTS_VALU"] * 64
-    ach = lane_instr / (launch_ms * 1e-3) / 1e12
-    cyc = c["GRBM_GUI_ACTIVE"] / 8  # summed over the 8 XCDs
-    out = {"bound": "valu", "achieved": round(ach, 3), "peak": round(VALU_PEAK_T, 3),
-           "unit": "T lane-instr/s", "frac": round(ach / VALU_PEAK_T, 4),
-           "valu_wave_instr_per_launch": int(c["SQ_INSTS_VALU"]),
-           "waves_per_launch": int(c["SQ_WAVES"]),
-           "source": os.path.relpath(VALU_PROFILE, REPO)}
-    out["valu_busy"] = round(c["SQ_INSTS_VALU"] * 2 / 1024 / cyc, 4)
+    path, prof = hit
+    rec = next((v for name, v in prof["kernels"].items() if name.startswith(kernel)), None)
+    if not rec or rec.get("read_bytes_x2") is None or rec.get("write_bytes") is None:
+        return None
+    return {"bytes": int(rec["read_bytes_x2"] + rec["write_bytes"]),
+            "read_bytes_x2": int(rec["read_bytes_x2"]), "write_bytes": int(rec["write_bytes"]),
+            "trace_avg_us": round(rec["avg_us"], 2), "source": os.path.relpath(path, REPO)}
+
+
+def blend_sq(config: str):
+    """Per-launch SQ counters of the blend from the config's committed profile, or None."""
+    hit = find_profile(config, "blend_sq")
+    if not hit:
+        return None
+    path, prof = hit
+    return prof["per_launch"], os.path.relpath(path, REPO)
+
+
+def blend_roofline(config, launch_ms, launch_ms_inflight, alg_bytes):
+    """The blend on the roof that bounds it: VALU (its exponent / composite chain; no dense
+    contraction, so no MFMA).  achieved = SQ_INSTS_VALU (wave64 instructions per launch, a
+    committed SQ profile of this build and config) x 64 lanes / the live launch time; peak =
+    256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz = 78.6 T lane-instructions/s (the 157.3 TFLOP/s FP32
+    vector peak counts an FMA as 2 flops; SQ_INSTS_VALU reads a calibration kernel's known count
+    exactly, profiles/r02_valu_calibration.md).  Beside it: the HBM roof from the counters
+    (FETCH_SIZE x2 + WRITE_SIZE per launch over the live launch time) and, as a labelled
+    diagnostic, SURVEY.md's algorithmic bytes 40 K + 12 W H over the launch time -- omitted when
+    above 1, which shows the blend does not read every pair's record (a pixel stops once T <
+    1e-4, a quadrant once its 64 pixels have)."""
+    out = {"bound": "valu", "kernel": "blend", "achieved": None, "peak": round(VALU_PEAK_T, 2),
+           "unit": "T lane-instr/s", "frac": None, "traffic": None,
+           "launch_ms": round(launch_ms, 5),
+           "launch_ms_source": "serial stage pass: HIP events around the kernel on the forward's "
+                               "stream, one frame at a time (the committed serial rocprofv3 "
+                               "trace agrees); achieved and frac use it",
+           "launch_ms_inflight": round(launch_ms_inflight, 5),
+           "launch_ms_inflight_source": "blend events of slot 0 in a separate untimed pass with "
+                                        "frames in flight"}
+    sq = blend_sq(config) if config else None
+    if sq:
+        c, src = sq
+        ach = c["SQ_INSTS_VALU"] * 64 / (launch_ms * 1e-3) / 1e12
+        cyc = c["GRBM_GUI_ACTIVE"] / 8  # summed over the 8 XCDs
+        out.update(achieved=round(ach, 3), frac=round(ach / VALU_PEAK_T, 4),
+                   valu_wave_instr_per_launch=int(c["SQ_INSTS_VALU"]),
+                   waves_per_launch=int(c["SQ_WAVES"]),
+                   valu_busy=round(c["SQ_INSTS_VALU"] * 2 / 1024 / cyc, 4), sq_source=src)
+    else:
+        out["note"] = "no committed SQ profile of this build and config: VALU achieved unmeasured"
+    tr = measured_traffic(config, BLEND_KERNEL) if config else None
+    if tr:
+        gbs = tr["bytes"] / (launch_ms * 1e-3) / 1e9
+        out["traffic"] = tr["bytes"]
+        out["hbm"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), **tr}
+    alg_frac = alg_bytes / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+    out["alg_bytes_diag"] = {"bytes_per_launch": int(alg_bytes),
+                             "frac_of_hbm": round(alg_frac, 4) if alg_frac <= 1.0 else None,
+                             "note": "SURVEY.md 8(d) 40 K + 12 W H: an upper bound on what the "
+                                     "blend must read, not a measurement" +
+                                     ("" if alg_frac <= 1.0 else
+                                      "; above 1 here, so not a bound (omitted)")}
     return out
 
 
@@ -193,16 +248,19 @@ def host_cpu():
     return model or platform.processor() or platform.machine(), env
 
 
-def cpu_baseline(scene, min_seconds):
-    """Two CPU legs on rank 0's host cores (the checker's code, timed here only as baselines):
+def cpu_baseline(scene, seconds):
+    """CPU legs on rank 0's host cores (the checker's code, timed here only as baselines):
 
     1. the reference's own CPU path -- the OpenGL backend's per-frame depth sort
        `_sort_gaussian_cpu` (renderer_ogl.py:10-19), as restated in `oracle.sort_gaussian_cpu`
        (bit-exact to outputs captured from the reference, tests/golden/sort_backend.npz), on the
        scene's P Gaussians and GL view: one warm-up, then the median of 5 calls;
-    2. the full forward on the CPU -- oracle/gsr_oracle.c, the C restatement of the upstream
-       rasterizer the viewer's CUDA backend calls (1 thread): whole frames of the same scene and
-       camera, at least 3 frames and at least min_seconds.  `value` is this leg's frame rate."""
+    2. the full forward on the host cores -- oracle/gsr_oracle.c, the C restatement of the
+       upstream rasterizer the viewer's CUDA backend calls, its loops parallel over OpenMP
+       threads (OMP_NUM_THREADS: the box's CPU share): whole frames of the same scene and
+       camera for `seconds` (at least one frame).  `value` is this leg's frame rate, `cores`
+       its thread count;
+    3. beside it, one frame of the same forward on one thread (scenes up to 2M Gaussians)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
     g = scene.host
@@ -214,25 +272,40 @@ def cpu_baseline(scene, min_seconds):
     sort_ms = 1e3 * float(np.median(ts[1:]))
     view, proj, campos = scene.cams[0][5]
     tx, ty = scene.cams[0][3], scene.cams[0][4]
-    frames, t0 = 0, time.perf_counter()
-    while True:
+
+    def frame():
         oracle.forward(g.xyz, g.opacity, view, proj, campos, tx, ty, scene.W, scene.H, shs=g.sh,
                        sh_degree=scene.deg, scales=g.scale, rotations=g.rot)
+
+    threads = oracle.set_threads(0)
+    frames, t0 = 0, time.perf_counter()
+    while True:
+        frame()
         frames += 1
         el = time.perf_counter() - t0
-        if el >= min_seconds and frames >= 3:
+        if el >= seconds:
             break
+    single = None
+    if scene.P <= 2_000_000:
+        oracle.set_threads(1)
+        t1 = time.perf_counter()
+        frame()
+        single = round(1.0 / (time.perf_counter() - t1), 5)
+        oracle.set_threads(0)
     model, env = host_cpu()
-    return {"value": round(frames / el, 5), "unit": "frames/sec", "cores": 1, "kind": "port",
+    return {"value": round(frames / el, 5), "unit": "frames/sec", "cores": threads, "kind": "port",
             "sample": f"{frames} full frame(s) of the {scene.P}-Gaussian {scene.W}x{scene.H} "
-                      f"SH{scene.deg} scene through oracle/gsr_oracle.c (1 thread, {el:.1f} s)",
+                      f"SH{scene.deg} scene through oracle/gsr_oracle.c on {threads} OpenMP "
+                      f"threads ({el:.1f} s)",
+            "single_thread_frames_per_sec": single,
             "reference_sort": {
                 "fn": "renderer_ogl._sort_gaussian_cpu (renderer_ogl.py:10-19) via "
                       "oracle.sort_gaussian_cpu, pinned to reference-captured outputs",
                 "ms_median_of_5": round(sort_ms, 3), "calls_per_sec": round(1e3 / sort_ms, 3),
                 "P": scene.P, "threads": "numpy argsort is single-threaded; the stacked matmul "
                                          "follows the BLAS / OpenMP env below"},
-            "host": {"cpu_model": model, "os_cpu_count": os.cpu_count(), "thread_env": env}}
+            "host": {"cpu_model": model, "os_cpu_count": os.cpu_count(),
+                     "affinity_cpus": len(os.sched_getaffinity(0)), "thread_env": env}}
 
 
 def main():
@@ -300,12 +373,6 @@ def main():
     for c in ctxs:
         opt = lambda o, v: _lib.check(lib.gsr_set_option(c, o, v), "gsr_set_option")  # noqa: E731
         opt(_lib.GSR_OPT_BLEND_FAST, {"exact": 0, "fast": 1}[args.blend])
-        if args.sort_shape is not None:
-            opt(_lib.GSR_OPT_TILE_SORT_SHAPE, args.sort_shape)
-        if args.inline_color:
-            opt(_lib.GSR_OPT_SPLIT_COLOR, 0)
-        if args.unfused:
-            opt(_lib.GSR_OPT_FUSED_BINNING, 0)
 
     # Warmup (also sizes the workspace so the timed loop never allocates).
     for i in range(args.warmup):
@@ -386,20 +453,14 @@ def main():
     sh_bytes = 4 * 3 * (scene.deg + 1) ** 2
     alg = algorithmic_bytes(P, P_f, P_v, K_mean, T_strip, W, rows_px, sh_bytes)
     # The roofline kernel is the blend: the largest share of GPU time in the rocprofv3 trace and
-    # the last kernel on the frame's critical path.  (The "color" stage's events span the whole
-    # second-stream interval -- pair count, SH colour and tile ranges, overlapped with the depth
-    # sort -- so its event time is not one kernel's launch duration.)
-    dominant = "blend" if stage_ms.get("blend", 0.0) > 0.0 else max(stage_ms, key=stage_ms.get)
-    # Launch duration for the roofline: the serial stage pass (one frame at a time, events on
-    # the forward's stream bracket the kernel alone), which is what a rocprofv3 kernel trace of
-    # a serial run reports for it (profiles/).  The timed region's blend events (two frames in
-    # flight) also count the other frame's kernels sharing the CUs; reported beside it.
-    dom_ms = stage_ms[dominant]
-    ach = alg[dominant] / (dom_ms * 1e-3) / 1e9
-    default_opts = not (args.sort_shape is not None or
-                        args.unfused or args.inline_color or
-                        args.blend != "fast")
-    traffic, traffic_src = measured_traffic(dominant, args.config, default_opts)
+    # the last kernel on the frame's critical path.  Its launch duration: the serial stage pass
+    # (one frame at a time, events on the forward's stream bracket the kernel alone), which is
+    # what the committed serial rocprofv3 trace reports for it; the timed region's blend events
+    # (two frames in flight, the other frame's kernels sharing the CUs) are reported beside it.
+    dom_ms = stage_ms["blend"]
+    roofline = blend_roofline(args.config if default_opts else None, dom_ms, blend_ms_timed,
+                              alg["blend"])
+    roofline["frame_alg_gbs"] = round(sum(alg.values()) / (t_max / args.steps) / 1e9, 2)
     fps = args.steps / t_max
     line = {
         "metric": METRIC,
@@ -413,9 +474,11 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (SURVEY.md §8(d) generator, seed %d; no PLY offline)" % CONFIGS[args.config][4],
-        "config": {"workload": f"{args.config}: {P} Gaussians, {W}x{H}, SH degree {scene.deg}, "
-                               f"{scene.cam_kind} camera",
+        "data": ("synthetic (%s, seed %d; no PLY offline)" %
+                 ("SURVEY.md §8(d) generator" if scene.generator == "uniform" else
+                  "gaussian_data.clustered_scene", CONFIGS[args.config][4])),
+        "config": {"workload": f"{args.config}: {P} Gaussians ({scene.generator} scene), {W}x{H}, "
+                               f"SH degree {scene.deg}, {scene.cam_kind} camera",
                    "gaussians": P, "width": W, "height": H, "sh_degree": scene.deg,
                    "parallelism": (f"SIMULATED strip {args.sim_strip} (diagnostic, no gather)"
                                    if args.sim_strip else
@@ -435,19 +498,7 @@ def main():
                                   "ranks all-reduce their tile rows' pair counts and re-split"}),
         "serial_ms_per_frame": round(serial_ms, 4),
         "serial_note": "one frame in flight at a time (no FramePipeline overlap), this rank",
-        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 2),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                     "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "bytes_per_launch": int(alg[dominant]),
-                     "launch_ms": round(dom_ms, 5),
-                     "launch_ms_source": "serial stage pass: HIP events around the kernel on "
-                                         "the forward's stream, one frame at a time; frac uses it",
-                     "launch_ms_inflight": round(blend_ms_timed, 5),
-                     "launch_ms_inflight_source": "blend events of slot 0 in a separate untimed "
-                                                  "pass with frames in flight",
-                     "frame_achieved_gbs": round(sum(alg.values()) / (t_max / args.steps) / 1e9, 2),
-                     "valu": valu_roofline(dominant, dom_ms, args.config, default_opts)},
+        "roofline": roofline,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

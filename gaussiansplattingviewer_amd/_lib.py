@@ -11,19 +11,14 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# GSR_LIB: another build of the library (A/B tuning builds); default the in-tree libgsr.so
+# GSR_LIB: another build of the library (A/B builds in tools/ab.sh); default the in-tree libgsr.so
 LIB_PATH = os.environ.get("GSR_LIB") or os.path.join(_HERE, "libgsr.so")
 ABI_VERSION = 1
 
 GSR_OPT_BLEND_CULL = 1
 GSR_OPT_BLEND_FAST = 2
-GSR_OPT_TILE_SORT_SHAPE = 4
-GSR_OPT_FUSED_BINNING = 5
-GSR_OPT_SPLIT_COLOR = 8
-GSR_OPT_PACKED_PAIRS = 9
 GSR_OPT_COLUMN_PAIRS = 10
 GSR_OPT_COMPACT_SORT = 11
-GSR_OPT_GRAPH = 12
 
 # Symbols include/gsr.h declares (checked by the CPU test suite).
 EXPORTED_SYMBOLS = (

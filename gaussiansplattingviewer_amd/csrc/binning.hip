@@ -118,55 +118,11 @@ __global__ __launch_bounds__(kBlock) void k_scan_down(const uint32_t *__restrict
     }
 }
 
-// Pass 4, upstream duplicateWithKeys, load-balanced by output: block c writes pairs
-// [c*kChunk, min(K, (c+1)*kChunk)) -- coalesced stores -- as (strip-local tile id, Gaussian
-// id), row-major over each Gaussian's rect like upstream.  The Gaussians overlapping the
-// chunk are staged in LDS; each output finds its owner by binary search over their offsets.
-__global__ __launch_bounds__(kBlock) void k_duplicate(
-    const uint4 *__restrict__ bin, const uint32_t *__restrict__ chunk_first, uint32_t K,
-    uint32_t n_chunks, uint32_t gx, uint32_t *__restrict__ tile_keys,
-    uint32_t *__restrict__ tile_vals) {
-    __shared__ uint32_t s_off[kChunk + 1];
-    __shared__ uint32_t s_id[kChunk + 1];
-    __shared__ uint32_t s_x0w[kChunk + 1];   // rect x0 | width << 16
-    __shared__ uint32_t s_row0[kChunk + 1];  // first strip-local tile row * gx
-    const int tid = threadIdx.x;
-    const uint32_t c = blockIdx.x;
-    const uint32_t e_end_all = chunk_first[n_chunks];
-    const uint32_t e0 = chunk_first[c];
-    const uint32_t e1 = (c + 1 < n_chunks) ? min(chunk_first[c + 1] + 1u, e_end_all) : e_end_all;
-    const int ne = (int)(e1 - e0);  // <= kChunk + 1: every staged Gaussian owns >= 1 pair
-    for (int i = tid; i < ne; i += kBlock) {
-        const uint4 b = bin[e0 + i];
-        s_off[i] = b.x;
-        s_id[i] = b.y;
-        s_x0w[i] = b.z;
-        s_row0[i] = b.w * gx;
-    }
-    __syncthreads();
-    const uint32_t o_end = min(K, (c + 1) * kChunk);
-    for (uint32_t o = c * kChunk + tid; o < o_end; o += kBlock) {
-        int lo = 0, hi = ne - 1;  // last staged Gaussian whose offset <= o
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_off[mid] <= o) lo = mid;
-            else hi = mid - 1;
-        }
-        const uint32_t local = o - s_off[lo];
-        const uint32_t x0w = s_x0w[lo];
-        const uint32_t width = x0w >> 16;
-        const uint32_t row = local / width;
-        const uint32_t col = local - row * width;
-        const uint32_t key = s_row0[lo] + row * gx + (x0w & 0xFFFFu) + col;
-        tile_keys[o] = key;
-        tile_vals[o] = s_id[lo];
-    }
-}
-
-// ---- fused duplicate + first tile-sort pass ------------------------------------------------
-// The tile sort's first radix pass needs, per sort tile, the digit histogram of its pairs and
-// then the pairs themselves in order.  Both are regenerated here from the depth-sorted
-// Gaussians instead of being written by k_duplicate and read back: k_dup_count builds the
+// ---- per-pair binning: upstream duplicateWithKeys fused with the first tile-sort pass ------
+// (The fallback for frames the column-first form below cannot take, api.hip.)  The tile sort's
+// first radix pass needs, per sort tile, the digit histogram of its pairs and then the pairs
+// themselves in order.  Both are generated here from the depth-sorted Gaussians instead of
+// being written by a duplicate kernel and read back: k_dup_count builds the
 // histogram of each 4096-pair output chunk (= one sort tile), k_rs_scan scans it, and
 // k_dup_scatter regenerates the chunk in registers, ranks it by the digit and scatters it --
 // the K-sized pair array is written once and never read by this pass.
@@ -320,7 +276,7 @@ __global__ __launch_bounds__(kFW * 64) void k_dup_scatter(
     const uint4 *__restrict__ bin, const uint32_t *__restrict__ chunk_first, uint32_t K,
     uint32_t n_chunks, uint32_t gx, int shift, int nbits, const uint32_t *__restrict__ hist,
     int64_t nb, const uint32_t *__restrict__ digit_total, uint32_t *__restrict__ keys_out,
-    uint32_t *__restrict__ vals_out, int pack_shift) {
+    uint32_t *__restrict__ vals_out) {
     union alignas(16) Smem {
         DupStage st;
         struct {
@@ -355,20 +311,12 @@ __global__ __launch_bounds__(kFW * 64) void k_dup_scatter(
         kk[j] = u.kv.keys[e];
         vv[j] = u.kv.vals[e];
     }
-    // packed pair list (pack_shift >= 0): one word per pair, the tile id bits the later
-    // passes sort on (above this pass's digit) over the Gaussian id; no key array is written
-    if (pack_shift >= 0) {
-#pragma unroll
-        for (int j = 0; j < kFIt; ++j)
-            vv[j] |= pack_shift < 32 ? (kk[j] >> (shift + nbits)) << pack_shift : 0u;
-    }
     // (radix_tile_scatter's first barrier orders these reads before its LDS writes)
     radix_tile_scatter<kFW, kFIt>(kk, vv, (int)(o_end - c * kFChunk), shift, nbits, hist, nb, c,
-                                  digit_total, pack_shift >= 0 ? nullptr : keys_out, vals_out,
-                                  sm, u.kv.keys, u.kv.vals);
+                                  digit_total, keys_out, vals_out, sm, u.kv.keys, u.kv.vals);
 }
 
-// ---- column-first pair generation (GSR_OPT_COLUMN_PAIRS) ----------------------------------
+// ---- column-first pair generation (the default binning; GSR_OPT_COLUMN_PAIRS) ------------------
 // The tile sort is LSD over (row, column): pass 1 by the column x, pass 2 by the row y.  Pass 1
 // needs no pair-level work: a Gaussian whose strip rect is [x0, x0+w) x [y0, y0+h) has h pairs
 // in each of its w columns, and in the stable column order those h pairs are contiguous (rows
@@ -493,8 +441,7 @@ __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict_
                                                      const uint32_t *__restrict__ d_n,
                                                      const uint32_t *__restrict__ hist, int64_t nb,
                                                      const uint32_t *__restrict__ digit_total,
-                                                     int pack_shift, uint32_t *__restrict__ out,
-                                                     uint32_t cap, uint32_t *__restrict__ d_K) {
+                                                     int pack_shift, uint32_t *__restrict__ out) {
     __shared__ ColScatterSmem c;
     __shared__ union {
         RadixTileSmem<kCW, kCIt> big;
@@ -513,14 +460,6 @@ __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict_
     uint32_t tot;
     // global start of column d for this block: all earlier columns, then earlier blocks
     const uint32_t dstart = block256_exclusive_scan(digit_total[tid], c.tmp, tot);
-    // tot = K, the frame's pair count.  A captured frame (api.hip) sized the pair buffers for
-    // `cap` before K was known: d_K = {K, 0} for the tile sort and the blend, or {0, 1} and no
-    // stores when K exceeds it (the host then grows the buffers and renders the frame again)
-    if (d_K && blockIdx.x == 0 && tid == 0) {
-        d_K[0] = tot <= cap ? tot : 0u;
-        d_K[1] = tot <= cap ? 0u : 1u;
-    }
-    if (tot > cap) return;  // block-uniform
     c.colbase[tid] = dstart + hist[(int64_t)tid * nb + blockIdx.x];
     // thread t owns segments [seg0, seg0 + w) (one per column of its rect)
     uint32_t nseg;
@@ -641,23 +580,12 @@ hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint2 *rect_sorted,
 
 int64_t gsr_duplicate_chunks(int64_t K) { return (K + kChunk - 1) / kChunk; }
 
-hipError_t gsr_launch_duplicate(const uint4 *bin, const uint32_t *chunk_first, int64_t K,
-                                uint32_t gx, uint32_t *tile_keys, uint32_t *tile_vals,
-                                hipStream_t s) {
-    const int64_t nc = gsr_duplicate_chunks(K);
-    if (nc == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_duplicate, dim3((unsigned)nc), dim3(kBlock), 0, s, bin, chunk_first,
-                       (uint32_t)K, (uint32_t)nc, gx, tile_keys, tile_vals);
-    return hipGetLastError();
-}
-
 int64_t gsr_fused_chunks(int64_t K) { return (K + kFChunk - 1) / kFChunk; }
 
 hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_first, int64_t K,
                                     uint32_t gx, int shift, int nbits, uint32_t *hist,
                                     uint32_t *digit_total, uint32_t *keys_out, uint32_t *vals_out,
-                                    uint2 *ranges_zero, uint32_t n_ranges, hipStream_t s,
-                                    int pack_shift) {
+                                    uint2 *ranges_zero, uint32_t n_ranges, hipStream_t s) {
     const int64_t nb = gsr_fused_chunks(K);
     if (nb == 0) return hipSuccess;
     const uint32_t nc = (uint32_t)gsr_duplicate_chunks(K);
@@ -668,7 +596,7 @@ hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_firs
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_dup_scatter, dim3((unsigned)nb), dim3(kFW * 64), 0, s, bin, chunk_first,
                        (uint32_t)K, nc, gx, shift, nbits, hist, nb, digit_total, keys_out,
-                       vals_out, pack_shift);
+                       vals_out);
     return hipGetLastError();
 }
 
@@ -864,10 +792,10 @@ hipError_t gsr_launch_col_pairs_count(const uint32_t *perm, const uint2 *strip_r
 hipError_t gsr_launch_col_pairs_scatter(const uint32_t *perm, const uint2 *rect_sorted,
                                         int64_t n_max, const uint32_t *d_n, const uint32_t *hist,
                                         const uint32_t *digit_total, int pack_shift, uint32_t *out,
-                                        hipStream_t s, uint32_t cap, uint32_t *d_K) {
+                                        hipStream_t s) {
     const int64_t nb = gsr_col_blocks(n_max);
     if (nb == 0) return hipSuccess;
     hipLaunchKernelGGL(k_col_scatter, dim3((unsigned)nb), dim3(kCG), 0, s, perm, rect_sorted, d_n,
-                       hist, nb, digit_total, pack_shift, out, cap, d_K);
+                       hist, nb, digit_total, pack_shift, out);
     return hipGetLastError();
 }

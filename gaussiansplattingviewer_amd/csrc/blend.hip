@@ -65,14 +65,14 @@ __device__ __forceinline__ bool may_touch(float x, float y, float A, float B, fl
     return !(lb > twoL);
 }
 
-// Block -> work item, XCD-aware: the hardware dispatches block b to XCD b % 8; groups of
-// `group` consecutive work items (a tile's quadrants and its row neighbours) go round-robin
-// over the XCDs, so each group shares one L2 while the image's heavy and light regions are
-// spread evenly over the 8 XCDs.  group = 0: plain order.
-__device__ __forceinline__ uint32_t xcd_work(uint32_t b, uint32_t group) {
-    if (group == 0) return b;
+// Block -> work item, XCD-aware: the hardware deals block b to XCD b % 8 (speed only, never
+// correctness); groups of kXcdGroup consecutive work items (four tiles' quadrants) go
+// round-robin over the XCDs, so each group shares one L2 while the image's heavy and light
+// regions are spread evenly over the 8 XCDs.
+constexpr uint32_t kXcdGroup = 16;
+__device__ __forceinline__ uint32_t xcd_work(uint32_t b) {
     const uint32_t x = b & 7u, l = b >> 3;
-    return ((l / group) * 8u + x) * group + l % group;
+    return ((l / kXcdGroup) * 8u + x) * kXcdGroup + l % kXcdGroup;
 }
 
 // One staged splat as the inner loop reads it: three 16-B LDS reads from one address (fast
@@ -104,8 +104,8 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
     constexpr bool kPair = kFast && !kContrib;  // paired colour / bound words (see staging)
 
     const uint32_t b = blockIdx.x;
-    const uint32_t work = xcd_work(b, a.xcd_group);
-    if (work >= n_work || (a.skip && *a.skip)) return;
+    const uint32_t work = xcd_work(b);
+    if (work >= n_work) return;
     const int lane = threadIdx.x;
     const uint32_t tile = work >> 2, quad = work & 3u;
     const uint32_t tx = tile % a.grid_x, ty_local = tile / a.grid_x, ty = a.row_begin + ty_local;
@@ -271,9 +271,9 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
     }
 }
 
-// Grid of whole XCD groups: n_work items, `group` per XCD round; blocks past n_work exit.
-inline uint32_t xcd_grid(uint32_t n_work, uint32_t group) {
-    const uint32_t g = group ? group * 8u : 8u;
+// Grid of whole XCD groups: n_work items, kXcdGroup per XCD round; blocks past n_work exit.
+inline uint32_t xcd_grid(uint32_t n_work) {
+    const uint32_t g = kXcdGroup * 8u;
     return (n_work + g - 1) / g * g;
 }
 
@@ -282,7 +282,7 @@ inline uint32_t xcd_grid(uint32_t n_work, uint32_t group) {
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s) {
     if (a.rows_tiles == 0 || a.grid_x == 0) return hipSuccess;
     const uint32_t n_work = 4u * a.grid_x * a.rows_tiles;
-    const dim3 grid(xcd_grid(n_work, a.xcd_group));
+    const dim3 grid(xcd_grid(n_work));
     if (a.fast && !a.n_contrib)
         hipLaunchKernelGGL((k_blend_q<true, false>), grid, dim3(64), 0, s, a, n_work);
     else if (a.fast)

@@ -372,20 +372,8 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
             pre += c[i];
         }
     }
-#if defined(GSR_DS_PROBE_STOP) && GSR_DS_PROBE_STOP == 1  // tools/micro/ds_probe.hip
-    {
-        uint32_t x = s_tab[tid * kDPer];
-        for (int j = 0; j < kDIt; ++j) x ^= k[j] ^ v[j];
-        if (x == 0x9E3779B9u) perm[0] = x;
-        return;
-    }
-#endif
     // every pass has >= 8 bits: sub-pass A takes 6, sub-pass B the remaining 6 or 2
     int kept = tile_rank_scatter<kDSub>(k, v, keep, shift, s_keys, s_vals, s_wcnt, s_tmp);
-#if defined(GSR_DS_PROBE_STOP) && GSR_DS_PROBE_STOP == 2
-    if (s_keys[tid] == 0x9E3779B9u) perm[0] = s_vals[tid];
-    return;
-#endif
     if (nbits > kDSub) {
         keep = 0u;
 #pragma unroll
@@ -410,10 +398,6 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
         if (i == 0 || ((s_keys[i - 1] >> shift) & mask) != d) s_tab[d] -= (uint32_t)i;
     }
     __syncthreads();
-#if defined(GSR_DS_PROBE_STOP) && GSR_DS_PROBE_STOP == 3
-    if (s_keys[tid] == 0x9E3779B9u) perm[0] = s_vals[tid] + s_tab[tid];
-    return;
-#endif
     for (int i = tid; i < kept; i += kDThreads) {
         const uint32_t kk = s_keys[i];
         const uint32_t g = s_tab[(kk >> shift) & mask] + (uint32_t)i;

@@ -217,21 +217,17 @@ struct GsrPreprocessArgs {
     // per k_preprocess block (ceil(P / 256)): its (Gaussian, strip tile) pair count, then as
     // many uint2 of the OR / AND of its kept depth keys
     uint64_t *block_pairs;
-    unsigned long long *host_K;  // pinned host memory (device-mapped): [K, D, -, tag, -, ktag]
-    const uint32_t *frame_tag;   // device word: this frame's tag, stored to host_K[3] after K
-    uint32_t k_tag;              // else (nonzero): stored to host_K[5] after K (the host spins)
+    unsigned long long *host_K;  // pinned host memory (device-mapped): [K, D, -, -, -, K tag]
+    uint32_t k_tag;              // nonzero: stored to host_K[5] after K (the host spins on it)
     // optional debug outputs
     float *depths, *means2D, *conic_opacity, *rgb;
     uint32_t *tiles_touched;
 };
 
-// with_color: evaluate the colour in the same kernel (else gsr_launch_color does it).
-hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, bool with_color, hipStream_t s);
-// SH -> RGB (or colors_precomp) of every Gaussian with radii > 0 into SplatRecord.c.yzw (+ rgb)
-// max_blocks > 0 caps the grid (grid-stride loop).
+hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, hipStream_t s);
+// SH -> RGB (or colors_precomp) of every Gaussian with radii > 0 into SplatRecord.c.yzw (+ rgb).
 // waves_per_simd (1..7): cap on the colour waves a CU holds at once (0 = no cap).
-hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, int waves_per_simd,
-                            hipStream_t s);
+hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int waves_per_simd, hipStream_t s);
 // Colour of the Gaussians listed in ids[0 .. *d_n) (the depth sort's compacted kept ids of a
 // strip frame), degree-3 16-B-aligned SH and no rgb output only (gsr_color_ids_ok).
 bool gsr_color_ids_ok(const GsrPreprocessArgs &a);
@@ -244,22 +240,20 @@ hipError_t gsr_launch_mark_visible(const float *means3D, int64_t P, const float 
                                    uint8_t *visible, hipStream_t s);
 hipError_t gsr_launch_view_depth_keys(const float *xyz, int64_t P, float v20, float v21, float v22,
                                       float v23, uint32_t *keys, float *depth_out, hipStream_t s);
-hipError_t gsr_launch_index_to_i32(const uint32_t *vals, int64_t P, int32_t *out, hipStream_t s);
 
-// Radix sort of (uint32 key, uint32 value) pairs, stable, LSD over key bits [begin, end).
-// On return *keys / *vals point at the buffers holding the sorted data (either the input
-// pair or the alt pair).  hist needs gsr_radix_hist_words(n) words.
+// Radix sort of (uint32 key, uint32 value) pairs, stable, LSD over key bits [begin, end) in
+// passes of <= 8 bits, starting at pass first_pass of that plan (the per-pair binning's first
+// pass runs fused with the duplication).  On return *keys / *vals point at the buffers holding
+// the sorted data (either the input pair or the alt pair).  hist needs gsr_radix_hist_words(n)
+// words, digit_total 256.
 int64_t gsr_radix_hist_words(int64_t n);
-// shape: tile shape (waves x items per lane): 0 = 4x16, 1 = 16x16, 2 = 4x8, 3 = 8x8, 4 = 8x16,
-// 5 = 4x4 (items per lane a multiple of 4, >= 4 waves).
-// d_count (compacting mode, >= 2 passes, first_pass 0): keys equal to 0xFFFFFFFF are dropped
-// by pass 0, the count of the others is stored at *d_count (device) and only they are sorted
-// -- the first *d_count entries of the result.  digit_total then needs 256 words per pass.
 hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
                                 uint32_t **vals_alt, int64_t n, int begin_bit, int end_bit,
                                 uint32_t *hist, uint32_t *digit_total, hipStream_t s,
-                                int shape = 0, int first_pass = 0, uint32_t *d_count = nullptr,
-                                const uint32_t *d_n = nullptr);
+                                int first_pass = 0);
+// The same for keys alone (the column-first binning's row pass over packed pair words).
+hipError_t gsr_radix_sort_keys(uint32_t **keys, uint32_t **keys_alt, int64_t n, int begin_bit,
+                               int end_bit, uint32_t *hist, uint32_t *digit_total, hipStream_t s);
 // k_rs_scan alone: per digit, exclusive scan of hist[d][0..nb) across tiles -> digit_total[d].
 hipError_t gsr_launch_digit_scan(uint32_t *hist, int64_t nb, uint32_t *digit_total,
                                  hipStream_t s);
@@ -322,9 +316,6 @@ hipError_t gsr_launch_scan_down(const uint32_t *perm, const uint2 *rect_sorted,
                                 const uint64_t *total, uint4 *bin, uint32_t *chunk_first,
                                 hipStream_t s);
 int64_t gsr_duplicate_chunks(int64_t K);
-hipError_t gsr_launch_duplicate(const uint4 *bin, const uint32_t *chunk_first, int64_t K,
-                                uint32_t gx, uint32_t *tile_keys, uint32_t *tile_vals,
-                                hipStream_t s);
 // Fused duplicate + first tile-sort radix pass (digit (key >> shift) & (2^nbits - 1)):
 // writes the K pairs, stably ordered by that digit, to keys_out / vals_out.  Uses
 // chunk_first as written by gsr_launch_scan_down; hist needs gsr_radix_hist_words(K) words.
@@ -332,8 +323,7 @@ int64_t gsr_fused_chunks(int64_t K);
 hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_first, int64_t K,
                                     uint32_t gx, int shift, int nbits, uint32_t *hist,
                                     uint32_t *digit_total, uint32_t *keys_out, uint32_t *vals_out,
-                                    uint2 *ranges_zero, uint32_t n_ranges, hipStream_t s,
-                                    int pack_shift = -1);
+                                    uint2 *ranges_zero, uint32_t n_ranges, hipStream_t s);
 // Column-first pair generation (binning.hip): pass 1 of the tile sort on (Gaussian, column)
 // segments of the depth-sorted Gaussians.  hist: gsr_col_blocks(n_max) * 256 words.
 int64_t gsr_col_blocks(int64_t n);
@@ -343,12 +333,11 @@ hipError_t gsr_launch_col_pairs_count(const uint32_t *perm, const uint2 *strip_r
 hipError_t gsr_launch_col_pairs_scatter(const uint32_t *perm, const uint2 *rect_sorted,
                                         int64_t n_max, const uint32_t *d_n, const uint32_t *hist,
                                         const uint32_t *digit_total, int pack_shift, uint32_t *out,
-                                        hipStream_t s, uint32_t cap = 0xFFFFFFFFu,
-                                        uint32_t *d_K = nullptr);
+                                        hipStream_t s);
 hipError_t gsr_launch_digit_scan_n(uint32_t *hist, int64_t nb, uint32_t *digit_total,
                                    const uint32_t *d_n, int64_t tile, hipStream_t s);
-// Packed pair lists (gsr_launch_dup_sort_pass with pack_shift >= 0): ids = packed & mask;
-// tile ids (offset + strip-local tile) from the tile ranges.
+// Packed pair lists (column-first binning): ids = packed & mask; tile ids (offset + strip-local
+// tile) from the tile ranges.
 hipError_t gsr_launch_unpack_ids(const uint32_t *packed, int64_t K, uint32_t mask, uint32_t *out,
                                  hipStream_t s);
 hipError_t gsr_launch_fill_tiles(const uint2 *ranges, uint32_t n_tiles, uint32_t offset,
@@ -386,8 +375,6 @@ struct GsrBlendArgs {
     uint32_t *n_contrib;
     int cull;            // 0: no quadrant cull (identical output, tested)
     int fast;            // 1: folded-constant FMA arithmetic + raw v_exp_f32; 0: upstream order
-    uint32_t xcd_group;  // work items per XCD round-robin group (0: plain block order)
     uint32_t id_mask;    // point_list word -> Gaussian id (packed pair lists; else ~0u)
-    const uint32_t *skip;  // captured frames: nonzero -> the pair list overflowed, draw nothing
 };
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s);

@@ -188,9 +188,7 @@ __device__ __forceinline__ float3 cull_data(float A, float B, float C, float o) 
     return make_float3((float)ex, (float)ey, __uint_as_float(__float_as_uint((float)Lm) + 1u));
 }
 
-// kColor: also evaluate the colour here (one kernel, no second stream).  Returns the number
-// of (Gaussian, strip tile) pairs of Gaussian idx.
-template <bool kColor>
+// Returns the number of (Gaussian, strip tile) pairs of Gaussian idx.
 __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, int64_t idx,
                                                    uint32_t &key_out) {
     int32_t radius_out = 0;
@@ -258,24 +256,7 @@ __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, i
                     rec.a = make_float4(px, py, conic_a, conic_b);
                     rec.b = make_float4(conic_c, opacity, cd.x, cd.y);
                 }
-                if (kColor) {
-                    float3 col;
-                    if (a.colors_precomp) {
-                        col = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1],
-                                          a.colors_precomp[3 * idx + 2]);
-                    } else {
-                        col = color_from_sh(p, a.campos, a.shs + idx * (int64_t)a.M * 3, a.D,
-                                            a.sh_vec4);
-                        if (a.rgb) {
-                            a.rgb[3 * idx] = col.x;
-                            a.rgb[3 * idx + 1] = col.y;
-                            a.rgb[3 * idx + 2] = col.z;
-                        }
-                    }
-                    if (strip_tiles) rec.c = make_float4(cd.z, col.x, col.y, col.z);
-                } else if (strip_tiles) {
-                    rec.c.x = cd.z;  // c.yzw: colour, written by k_color
-                }
+                if (strip_tiles) rec.c.x = cd.z;  // c.yzw: the colour, written by k_color
                 if (a.depths) a.depths[idx] = p_view.z;
                 if (a.means2D) {
                     a.means2D[2 * idx] = px;
@@ -300,11 +281,10 @@ __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, i
 // K sizes the binning, bits(OR ^ AND) the depth sort's passes), and with a.block_kept (the
 // depth sort's compaction, strips) how many of its 256 Gaussians have pairs in the strip.
 // (A separate pass re-reading the rects and keys took 7 us at C3 and 42 us on a C4 strip.)
-template <bool kColor>
 __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t key = 0xFFFFFFFFu;
-    const uint32_t pairs = idx < a.P ? preprocess_one<kColor>(a, idx, key) : 0u;
+    const uint32_t pairs = idx < a.P ? preprocess_one(a, idx, key) : 0u;
     const bool kept = pairs != 0u;  // has pairs in the strip <=> its depth key is kept
     uint32_t v = pairs, o = kept ? key : 0u, an = kept ? key : 0xFFFFFFFFu;  // v <= 256 x 2^16
 #pragma unroll
@@ -337,7 +317,6 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
 __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__restrict__ cnt,
                                                     const uint2 *__restrict__ keybits, int64_t n,
                                                     unsigned long long *host_K,
-                                                    const uint32_t *__restrict__ frame_tag,
                                                     uint32_t k_tag) {
     __shared__ unsigned long long s_w[16];
     __shared__ uint32_t s_or[16], s_and[16];
@@ -373,12 +352,9 @@ __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__
         const unsigned long long D = diff ? 32u - (uint32_t)__clz(diff) : 0u;
         __hip_atomic_store(host_K + 1, D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(host_K, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        // a captured frame's host waits for this tag (release: K and D are visible first)
-        if (frame_tag)
-            __hip_atomic_store(host_K + 3, (unsigned long long)*frame_tag, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        // a stream frame's host spins on this tag instead of sleeping in an event wait
-        else if (k_tag)
+        // the host spins on this tag instead of sleeping in an event wait (release: K and D are
+        // visible first)
+        if (k_tag)
             __hip_atomic_store(host_K + 5, (unsigned long long)k_tag, __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -501,35 +477,23 @@ __global__ __launch_bounds__(256) void k_view_depth_keys(const float *__restrict
     if (depth_out) depth_out[idx] = d;
 }
 
-__global__ __launch_bounds__(256) void k_index_to_i32(const uint32_t *vals, int64_t P,
-                                                      int32_t *out) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx < P) out[idx] = (int32_t)vals[idx];
-}
-
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace
 
-hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, bool with_color, hipStream_t s) {
+hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, hipStream_t s) {
     if (a.P == 0) return hipSuccess;
-    if (with_color)
-        hipLaunchKernelGGL(k_preprocess<true>, dim3(grid_for(a.P)), dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(k_preprocess<false>, dim3(grid_for(a.P)), dim3(256), 0, s, a);
-
+    hipLaunchKernelGGL(k_preprocess, dim3(grid_for(a.P)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, int waves_per_simd,
-                            hipStream_t s) {
+hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int waves_per_simd, hipStream_t s) {
     if (a.P == 0) return hipSuccess;
     const unsigned g0 = grid_for(a.P);  // 4 waves of 64 Gaussians per block
     if (!a.sh_vec4 || a.colors_precomp || a.D != 3) {
         hipLaunchKernelGGL(k_color_generic, dim3(g0), dim3(256), 0, s, a);
         return hipGetLastError();
     }
-    const unsigned g = max_blocks > 0 && (unsigned)max_blocks < g0 ? max_blocks : g0;
     // a 4-wave block puts one wave on each SIMD: w blocks per CU = w waves per SIMD, held by
     // reserving 1/w of the CU's 160 KiB of LDS per block (1 KiB granules)
     size_t lds = 0;
@@ -542,7 +506,7 @@ hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int max_blocks, int wave
             if (e != hipSuccess) return e;
         }
     }
-    hipLaunchKernelGGL(k_color, dim3(g), dim3(256), lds, s, a);
+    hipLaunchKernelGGL(k_color, dim3(g0), dim3(256), lds, s, a);
     return hipGetLastError();
 }
 
@@ -567,7 +531,7 @@ hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s) {
     const uint2 *keybits = reinterpret_cast<const uint2 *>(a.block_pairs + g);
     hipLaunchKernelGGL(k_publish_K, dim3(1), dim3(1024), 0, s,
                        reinterpret_cast<const unsigned long long *>(a.block_pairs), keybits,
-                       (int64_t)g, a.host_K, a.frame_tag, a.k_tag);
+                       (int64_t)g, a.host_K, a.k_tag);
     return hipGetLastError();
 }
 
@@ -584,11 +548,5 @@ hipError_t gsr_launch_view_depth_keys(const float *xyz, int64_t P, float v20, fl
     if (P == 0) return hipSuccess;
     hipLaunchKernelGGL(k_view_depth_keys, dim3(grid_for(P)), dim3(256), 0, s, xyz, P, v20, v21,
                        v22, v23, keys, depth_out);
-    return hipGetLastError();
-}
-
-hipError_t gsr_launch_index_to_i32(const uint32_t *vals, int64_t P, int32_t *out, hipStream_t s) {
-    if (P == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_index_to_i32, dim3(grid_for(P)), dim3(256), 0, s, vals, P, out);
     return hipGetLastError();
 }

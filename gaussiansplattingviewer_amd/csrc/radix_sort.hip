@@ -25,62 +25,31 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kRadix = kRadixBins;
 
-// Element count of a pass.  The compacting depth sort (gsr_radix_sort_compact) learns its
-// count on the device: pass 0 drops the sentinel keys, pass 1's upsweep sums pass 0's digit
-// totals (sum_digits; block 0 stores the sum at n_out) and every later kernel reads it from
-// d_n.  Grids and the hist column stride stay sized for the host's upper bound.
+// Element count of a pass: n_host, or *d_n when set (the column-first binning's scan learns
+// its live block count from the depth sort's kept count on the device).  Grids and the hist
+// column stride stay sized for n_host.
 struct RsCount {
     int64_t n_host;
-    const uint32_t *sum_digits;  // if set: n = sum of these 256 words
-    uint32_t *n_out;             // with sum_digits: block 0 stores n here
-    const uint32_t *d_n;         // else if set: n = *d_n
+    const uint32_t *d_n;
 };
 
-// All threads of the block call it (the sum_digits form reduces over 256 threads).
-template <int kThreads>
-__device__ __forceinline__ int64_t resolve_count(const RsCount &c, uint32_t *s_red) {
-    if (c.sum_digits) {
-        static_assert(kThreads >= kRadixBins, "one thread per digit");
-        const int tid = threadIdx.x;
-        uint32_t v = tid < kRadixBins ? c.sum_digits[tid] : 0u;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if ((tid & 63) == 0) s_red[tid >> 6] = v;
-        __syncthreads();
-        uint32_t n = 0;
-#pragma unroll
-        for (int i = 0; i < kThreads / 64; ++i) n += s_red[i];
-        __syncthreads();
-        if (c.n_out && blockIdx.x == 0 && tid == 0) *c.n_out = n;
-        return n;
-    }
-    if (c.d_n) return *c.d_n;
-    return c.n_host;
-}
-
-// Reduce-then-scan, parameterised by waves per block (kW = 4: 4096-key tiles for the
-// P-sized depth sort; kW = 16: 16384-key tiles and 1024-thread blocks for the K-sized tile
-// sort, so each digit's run in a tile is long enough for full-line stores).  nb = hist column
-// stride (tiles of the host's upper bound); kDrop: keys equal to kDropKey are not counted.
-template <int kW, int kIt, bool kDrop = false>
+// Reduce-then-scan over tiles of kW waves x kIt keys per lane (8 x 8 = 4096 keys: the fastest
+// shape measured for the K-sized tile sort).  nb = hist column stride (tiles of the
+// host's upper bound).
+template <int kW, int kIt>
 __global__ __launch_bounds__(kW * 64) void k_rs_upsweep(const uint32_t *__restrict__ keys,
-                                                        const RsCount cnt, int shift,
-                                                        uint32_t mask,
+                                                        int64_t n, int shift, uint32_t mask,
                                                         uint32_t *__restrict__ hist, int64_t nb) {
     constexpr int kThreads = kW * 64, kT = kThreads * kIt;
     static_assert(kIt % 4 == 0, "full tiles are read as uint4");
     static_assert(kW >= 4, "the digit scans take one thread per digit (256)");
     __shared__ uint32_t s_hist[kW][kRadix];
-    __shared__ uint32_t s_red[kW];
     const int tid = threadIdx.x, w = tid >> 6;
-    const int64_t n = resolve_count<kThreads>(cnt, s_red);
     const int64_t base = (int64_t)blockIdx.x * kT;
     if (base >= n) return;  // whole block (the scan reads columns [0, ceil(n / kT)) only)
     for (int i = tid; i < kW * kRadix; i += kThreads) (&s_hist[0][0])[i] = 0;
     __syncthreads();
-    auto add = [&](uint32_t key) {
-        if (!kDrop || key != kDropKey) atomicAdd(&s_hist[w][(key >> shift) & mask], 1u);
-    };
+    auto add = [&](uint32_t key) { atomicAdd(&s_hist[w][(key >> shift) & mask], 1u); };
     if (base + kT <= n) {
         const uint4 *k4 = reinterpret_cast<const uint4 *>(keys + base);
 #pragma unroll
@@ -135,10 +104,10 @@ __global__ __launch_bounds__(kBlock) void k_rs_scan(uint32_t *__restrict__ hist,
 
 // kVals = false: keys only (vals_in / vals_out unused) -- no LDS for values, so more blocks
 // share a CU.
-template <int kW, int kIt, bool kDrop = false, bool kVals = true>
+template <int kW, int kIt, bool kVals>
 __global__ __launch_bounds__(kW * 64) void k_rs_downsweep(
     const uint32_t *__restrict__ keys_in, const uint32_t *__restrict__ vals_in,
-    uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out, const RsCount cnt,
+    uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out, int64_t n,
     int shift, int nbits, const uint32_t *__restrict__ hist,
     const uint32_t *__restrict__ digit_total, int64_t nb) {
     constexpr int kT = kW * 64 * kIt;
@@ -146,7 +115,6 @@ __global__ __launch_bounds__(kW * 64) void k_rs_downsweep(
     __shared__ uint32_t s_vals[kVals ? kT : 1];
     __shared__ RadixTileSmem<kW, kIt> sm;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t n = cnt.d_n ? (int64_t)*cnt.d_n : cnt.n_host;
     const int64_t base = (int64_t)blockIdx.x * kT;
     if (base >= n) return;  // whole block
     uint32_t k[kIt], v[kIt];
@@ -158,7 +126,7 @@ __global__ __launch_bounds__(kW * 64) void k_rs_downsweep(
         v[j] = (kVals && valid) ? vals_in[e] : 0u;
     }
     const int64_t rem = n - base;
-    radix_tile_scatter<kW, kIt, kDrop>(k, v, rem < kT ? (int)rem : kT, shift, nbits, hist, nb,
+    radix_tile_scatter<kW, kIt>(k, v, rem < kT ? (int)rem : kT, shift, nbits, hist, nb,
                                        blockIdx.x, digit_total, keys_out,
                                        kVals ? vals_out : nullptr, sm, s_keys, s_vals);
 }
@@ -183,7 +151,7 @@ GsrRadixPlan gsr_radix_plan(int begin_bit, int end_bit) {
 hipError_t gsr_launch_digit_scan(uint32_t *hist, int64_t nb, uint32_t *digit_total,
                                  hipStream_t s) {
     hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, nb, digit_total,
-                       RsCount{nb, nullptr, nullptr, nullptr}, (int64_t)1);
+                       RsCount{nb, nullptr}, (int64_t)1);
     return hipGetLastError();
 }
 
@@ -191,79 +159,61 @@ hipError_t gsr_launch_digit_scan(uint32_t *hist, int64_t nb, uint32_t *digit_tot
 hipError_t gsr_launch_digit_scan_n(uint32_t *hist, int64_t nb, uint32_t *digit_total,
                                    const uint32_t *d_n, int64_t tile, hipStream_t s) {
     hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, nb, digit_total,
-                       RsCount{nb, nullptr, nullptr, d_n}, tile);
+                       RsCount{nb, d_n}, tile);
     return hipGetLastError();
 }
 
+namespace {
+constexpr int kSW = 8, kSIt = 8;  // sort tile: 8 waves x 8 keys per lane
+constexpr int64_t kST = (int64_t)kSW * 64 * kSIt;
+}  // namespace
+
 int64_t gsr_radix_hist_words(int64_t n) {
-    const int64_t nb = (n + 1023) / 1024;  // smallest tile shape (4 waves x 4 items)
+    const int64_t nb = (n + kST - 1) / kST;
     return (nb < 1 ? 1 : nb) * kRadix;
 }
 
-template <int kW, int kIt, bool kDrop = false>
-static void rts_pass(const uint32_t *k, const uint32_t *v, uint32_t *ko, uint32_t *vo,
-                     const RsCount &up_cnt, const RsCount &cnt, int shift, int nbits,
-                     uint32_t *hist, uint32_t *digit_total, hipStream_t s) {
-    const int64_t kT = (int64_t)kW * 64 * kIt;
-    const int64_t nb = (cnt.n_host + kT - 1) / kT;  // grid and hist column stride
+// One pass: upsweep, scan, downsweep.  v == nullptr: keys only.
+static void rts_pass(const uint32_t *k, const uint32_t *v, uint32_t *ko, uint32_t *vo, int64_t n,
+                     int shift, int nbits, uint32_t *hist, uint32_t *digit_total, hipStream_t s) {
+    const int64_t nb = (n + kST - 1) / kST;  // grid and hist column stride
     if (nb == 0) return;
     const uint32_t mask = (1u << nbits) - 1u;
-    hipLaunchKernelGGL((k_rs_upsweep<kW, kIt, kDrop>), dim3((unsigned)nb), dim3(kW * 64), 0, s,
-                       k, up_cnt, shift, mask, hist, nb);
-    hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, nb, digit_total, cnt,
-                       kT);
+    hipLaunchKernelGGL((k_rs_upsweep<kSW, kSIt>), dim3((unsigned)nb), dim3(kSW * 64), 0, s, k, n,
+                       shift, mask, hist, nb);
+    hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, nb, digit_total,
+                       RsCount{nb, nullptr}, kST);
     if (v)
-        hipLaunchKernelGGL((k_rs_downsweep<kW, kIt, kDrop, true>), dim3((unsigned)nb),
-                           dim3(kW * 64), 0, s, k, v, ko, vo, cnt, shift, nbits, hist,
-                           digit_total, nb);
+        hipLaunchKernelGGL((k_rs_downsweep<kSW, kSIt, true>), dim3((unsigned)nb), dim3(kSW * 64), 0,
+                           s, k, v, ko, vo, n, shift, nbits, hist, digit_total, nb);
     else
-        hipLaunchKernelGGL((k_rs_downsweep<kW, kIt, kDrop, false>), dim3((unsigned)nb),
-                           dim3(kW * 64), 0, s, k, v, ko, vo, cnt, shift, nbits, hist,
-                           digit_total, nb);
-}
-
-template <int kW, int kIt>
-static void rts_sort(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt, uint32_t **vals_alt,
-                     int64_t n, const GsrRadixPlan &plan, int first_pass, uint32_t *hist,
-                     uint32_t *digit_total, uint32_t *d_count, const uint32_t *d_n,
-                     hipStream_t s) {
-    for (int p = first_pass; p < plan.n; ++p) {
-        const int sh = plan.shift[p], nbits = plan.nbits[p];
-        if (!d_count) {  // n: grids and hist stride; d_n (if set): the live count, on the device
-            const RsCount c{n, nullptr, nullptr, d_n};
-            rts_pass<kW, kIt>(*keys, *vals, *keys_alt, *vals_alt, c, c, sh, nbits, hist,
-                              digit_total, s);
-        } else if (p == 0) {  // drop the sentinel keys; pass 0's digit totals sum to the count
-            const RsCount c{n, nullptr, nullptr, nullptr};
-            rts_pass<kW, kIt, true>(*keys, *vals, *keys_alt, *vals_alt, c, c, sh, nbits, hist,
-                                    digit_total, s);
-        } else {  // pass 1's upsweep stores the count; everything else reads it
-            const RsCount up = p == 1 ? RsCount{n, digit_total, d_count, nullptr}
-                                      : RsCount{n, nullptr, nullptr, d_count};
-            const RsCount c{n, nullptr, nullptr, d_count};
-            rts_pass<kW, kIt>(*keys, *vals, *keys_alt, *vals_alt, up, c, sh, nbits, hist,
-                              digit_total + kRadix * p, s);
-        }
-        std::swap(*keys, *keys_alt);
-        std::swap(*vals, *vals_alt);  // (keys-only sorts pass pointers to null pointers)
-    }
+        hipLaunchKernelGGL((k_rs_downsweep<kSW, kSIt, false>), dim3((unsigned)nb), dim3(kSW * 64),
+                           0, s, k, v, ko, vo, n, shift, nbits, hist, digit_total, nb);
 }
 
 hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
                                 uint32_t **vals_alt, int64_t n, int begin_bit, int end_bit,
-                                uint32_t *hist, uint32_t *digit_total, hipStream_t s, int shape,
-                                int first_pass, uint32_t *d_count, const uint32_t *d_n) {
-    if (n <= 1 && !d_count && !d_n) return hipSuccess;
+                                uint32_t *hist, uint32_t *digit_total, hipStream_t s,
+                                int first_pass) {
+    if (n <= 1) return hipSuccess;
     const GsrRadixPlan plan = gsr_radix_plan(begin_bit, end_bit);
-    if (d_count && (d_n || plan.n < 2 || first_pass != 0))
-        return hipErrorInvalidValue;  // the count is established by passes 0 and 1
-    switch (shape) {
-        case 1: rts_sort<16, 16>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, d_n, s); break;
-        case 2: rts_sort<4, 8>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, d_n, s); break;
-        case 3: rts_sort<8, 8>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, d_n, s); break;
-        case 4: rts_sort<8, 16>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, d_n, s); break;
-        case 5: rts_sort<4, 4>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, d_n, s); break;
-        default: rts_sort<4, 16>(keys, vals, keys_alt, vals_alt, n, plan, first_pass, hist, digit_total, d_count, d_n, s); break;
+    for (int p = first_pass; p < plan.n; ++p) {
+        rts_pass(*keys, *vals, *keys_alt, *vals_alt, n, plan.shift[p], plan.nbits[p], hist,
+                 digit_total, s);
+        std::swap(*keys, *keys_alt);
+        std::swap(*vals, *vals_alt);
+    }
+    return hipGetLastError();
+}
+
+hipError_t gsr_radix_sort_keys(uint32_t **keys, uint32_t **keys_alt, int64_t n, int begin_bit,
+                               int end_bit, uint32_t *hist, uint32_t *digit_total, hipStream_t s) {
+    if (n <= 1) return hipSuccess;
+    const GsrRadixPlan plan = gsr_radix_plan(begin_bit, end_bit);
+    for (int p = 0; p < plan.n; ++p) {
+        rts_pass(*keys, nullptr, *keys_alt, nullptr, n, plan.shift[p], plan.nbits[p], hist,
+                 digit_total, s);
+        std::swap(*keys, *keys_alt);
     }
     return hipGetLastError();
 }

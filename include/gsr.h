@@ -24,8 +24,9 @@
  *   - matrices passed as device pointers are 16 floats, column-major (upstream's layout,
  *     i.e. the row-major bytes of `view.T` that renderer_cuda.py:192-194 uploads);
  *   - `stream` is a hipStream_t (NULL = the default stream); all work is enqueued on it.
- *     gsr_forward synchronises that stream once per call to read back the number of
- *     (Gaussian, tile) pairs, as upstream does for num_rendered;
+ *     gsr_forward waits once per call for the number of (Gaussian, tile) pairs, as upstream
+ *     does for num_rendered -- not for the stream: the GPU stores it into pinned memory as
+ *     soon as the preprocess has counted it, while the depth sort runs;
  *   - every function returns GSR_OK (0) or a negative GSR_E* code; gsr_last_error()
  *     returns the calling thread's last message.  The Python layer raises RuntimeError.
  */
@@ -195,51 +196,24 @@ int gsr_set_timing(gsr_context *ctx, int enable);
 int gsr_stage_times(gsr_context *ctx, float *ms, int n);
 const char *gsr_stage_name(int i);
 
-/* Tuning / verification switches.
+/* Options (per context; every setting renders the same binning, and the blend options change
+ * pixels by float rounding at most -- tests/test_gpu_parity.py checks each):
  *   GSR_OPT_BLEND_CULL (default 1): conservative ellipse-vs-quadrant cull in the blend;
- *     outputs are bit-identical either way (tested).
+ *     outputs are bit-identical either way.
  *   GSR_OPT_BLEND_FAST (default 1): blend arithmetic with log2(e) folded into the conic, FMA
- *     contraction and the hardware exp2; changes pixels by float rounding only (tolerance in
- *     tests/gpu_helpers.py).  0 keeps upstream's per-pixel operation order (IEEE, no FMA,
- *     ocml expf). */
-/*   GSR_OPT_TILE_SORT_SHAPE (tuning): tile shape of the pair sort's reduce-then-scan kernels,
- *     0 = 4 waves x 16 keys/lane, 1 = 16x16, 2 = 4x8, 3 = 8x8 (default), 4 = 8x16, 5 = 4x4.
- *     (Option ids 3, 6 and 7 -- the onesweep sort, the 4-wave blend blocks and the old
- *     depth-sort shape -- are retired.) */
-/*   GSR_OPT_FUSED_BINNING (default 1): the pair duplication regenerates each 4096-pair chunk
- *     and performs the tile sort's first radix pass in the same kernel (reduce-then-scan
- *     sort only); 0 = separate duplicate kernel + full sort.  Identical results. */
-/*   GSR_OPT_SPLIT_COLOR (default 1): SH -> RGB runs as its own kernel on an internal second
- *     stream, overlapped with the depth sort and the binning; 0 = inside the preprocess
- *     kernel.  Identical results. */
-/*   GSR_OPT_PACKED_PAIRS (default 1): the (tile, Gaussian) pair list is one 32-bit word per
- *     pair -- the tile-id bits the second tile-sort pass needs above the Gaussian id --
- *     written once by the fused duplicate and sorted keys-only; used when the tile ranges come
- *     from the second stream and the bits fit (P <= 2^(32 - second-pass bits)), else key and
- *     value arrays.  Identical results. */
-/*   GSR_OPT_COLUMN_PAIRS (default 1): the first tile-sort pass (by tile column) runs on
- *     (Gaussian, column) segments of the depth-sorted Gaussians -- a per-column difference-
- *     array count and a segment scatter -- instead of regenerating and ranking every pair; the
- *     second pass sorts packed (tile row, Gaussian id) words.  Needs the second-stream ranges,
- *     <= 256 tile columns and rows per strip, P <= 2^(32 - row bits).  Identical results. */
-/*   GSR_OPT_COMPACT_SORT (default -1 = auto): 1 = the depth sort first compacts the keys of
- *     the Gaussians with pairs in the strip (per-block counts from the preprocess, a scan, an
- *     ordered scatter) and sorts only those; 0 = pass 0 drops the others while it sorts; auto =
- *     compact on strips (tile_row_begin/end a proper subset) of >= 4M Gaussians, where most
- *     keys are dropped and pass 0 is long.  Identical results. */
-/*   GSR_OPT_GRAPH (default 0): a forward that uses the column-first binning (the default
- *     path) is recorded once as a hipGraph per distinct set of inputs / outputs / options and
- *     replayed: per frame one camera-staging launch, one graph launch and a wait for the pair
- *     count K in pinned memory, instead of ~20 launches and the event hand-offs.  The pair
- *     buffers are sized 25 % above the last K; a frame whose K exceeds them is detected on the
- *     device (binning and blend skipped) and rendered again on the stream after growing them.
- *     Not used while stage timing or debug is on.  Identical results.  Off by default: the
- *     recorded frame is one stream (ROCm launches fork / join graphs ~10x slower), which
- *     costs more GPU time than the host time it saves. */
-enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2,
-       GSR_OPT_TILE_SORT_SHAPE = 4, GSR_OPT_FUSED_BINNING = 5,
-       GSR_OPT_SPLIT_COLOR = 8, GSR_OPT_PACKED_PAIRS = 9, GSR_OPT_COLUMN_PAIRS = 10,
-       GSR_OPT_COMPACT_SORT = 11, GSR_OPT_GRAPH = 12 };
+ *     contraction and the hardware exp2 (tolerance in tests/gpu_helpers.py); 0 keeps upstream's
+ *     per-pixel operation order (IEEE, no FMA, ocml expf).
+ *   GSR_OPT_COLUMN_PAIRS (default 1): column-first binning -- the first tile-sort pass runs on
+ *     (Gaussian, tile column) segments of the depth-sorted Gaussians and the second sorts packed
+ *     (tile row, Gaussian id) words, with the tile ranges from the rects on a second stream.
+ *     Frames it cannot take (> 256 tile columns or strip rows, more Gaussians than the packed
+ *     word holds) use the per-pair form; 0 forces the per-pair form.
+ *   GSR_OPT_COMPACT_SORT (default -1 = auto): 1 = the depth sort first compacts the keys of the
+ *     Gaussians with pairs in the strip and sorts only those; 0 = its first pass drops the others
+ *     while it sorts; auto = compact on strips (a proper subset of the tile rows) of >= 4M
+ *     Gaussians. */
+enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_COLUMN_PAIRS = 10,
+       GSR_OPT_COMPACT_SORT = 11 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
 
 #ifdef __cplusplus

@@ -35,8 +35,15 @@
  * division and sqrt, evaluation order exactly as written in upstream C++ (left-to-right
  * sums, glm column-major mat3 products).  ndc2Pix evaluates in double because upstream's
  * literals 1.0 / 0.5 are doubles.
+ *
+ * Threads (OpenMP, oracle_set_threads; for the bench's host-cores CPU baseline): the
+ * preprocess runs Gaussians in parallel, the duplication fills each Gaussian's precomputed
+ * range, the stable LSD sort counts and scatters per contiguous chunk (chunk-ordered offsets
+ * keep it stable), and the render runs tiles in parallel.  Every output element is computed by
+ * the same operations as in the serial order, so results do not depend on the thread count.
  */
 #include <math.h>
+#include <omp.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -246,6 +253,7 @@ int64_t oracle_preprocess(const OracleIn *in, float *depths, int32_t *radii, flo
     const float focal_y = in->H / (2.0f * in->tanfovy);
     const float focal_x = in->W / (2.0f * in->tanfovx);
     int64_t K = 0;
+#pragma omp parallel for schedule(static, 4096) reduction(+ : K)
     for (int64_t idx = 0; idx < in->P; ++idx) {
         radii[idx] = 0;
         tiles_touched[idx] = 0;
@@ -324,22 +332,42 @@ static uint32_t get_higher_msb(uint32_t n) {
 }
 
 /* Stable LSD radix sort of (key, value) on key bits [0, end_bit): the contract of
- * cub::DeviceRadixSort::SortPairs as rasterizer_impl.cu calls it. */
+ * cub::DeviceRadixSort::SortPairs as rasterizer_impl.cu calls it.  8-bit digits; each pass
+ * counts per contiguous chunk (one per thread), offsets digit-major then chunk-major, and
+ * every chunk scatters its elements in order -- the stable counting sort, in parallel. */
+#define SORT_MAX_CHUNKS 256
 static int sort_pairs_u64(uint64_t *keys, uint32_t *vals, int64_t n, int end_bit) {
     uint64_t *k2 = (uint64_t *)malloc((size_t)(n > 0 ? n : 1) * sizeof(uint64_t));
     uint32_t *v2 = (uint32_t *)malloc((size_t)(n > 0 ? n : 1) * sizeof(uint32_t));
-    if (!k2 || !v2) { free(k2); free(v2); return -1; }
+    int64_t(*cnt)[256] = malloc(sizeof(int64_t[256]) * SORT_MAX_CHUNKS);
+    if (!k2 || !v2 || !cnt) { free(k2); free(v2); free(cnt); return -1; }
+    int nch = omp_get_max_threads();
+    if (nch > SORT_MAX_CHUNKS) nch = SORT_MAX_CHUNKS;
+    if (nch < 1 || n < 65536) nch = 1;
     uint64_t *ka = keys, *kb = k2;
     uint32_t *va = vals, *vb = v2;
     for (int shift = 0; shift < end_bit; shift += 8) {
-        int64_t cnt[257];
-        memset(cnt, 0, sizeof(cnt));
-        for (int64_t i = 0; i < n; ++i) cnt[((ka[i] >> shift) & 0xFF) + 1]++;
-        for (int d = 0; d < 256; ++d) cnt[d + 1] += cnt[d];
-        for (int64_t i = 0; i < n; ++i) {
-            const int64_t pos = cnt[(ka[i] >> shift) & 0xFF]++;
-            kb[pos] = ka[i];
-            vb[pos] = va[i];
+#pragma omp parallel for num_threads(nch) schedule(static, 1)
+        for (int c = 0; c < nch; ++c) {
+            const int64_t b = n * c / nch, e = n * (c + 1) / nch;
+            memset(cnt[c], 0, sizeof(cnt[c]));
+            for (int64_t i = b; i < e; ++i) cnt[c][(ka[i] >> shift) & 0xFF]++;
+        }
+        int64_t run = 0;
+        for (int d = 0; d < 256; ++d)
+            for (int c = 0; c < nch; ++c) {
+                const int64_t t = cnt[c][d];
+                cnt[c][d] = run;
+                run += t;
+            }
+#pragma omp parallel for num_threads(nch) schedule(static, 1)
+        for (int c = 0; c < nch; ++c) {
+            const int64_t b = n * c / nch, e = n * (c + 1) / nch;
+            for (int64_t i = b; i < e; ++i) {
+                const int64_t pos = cnt[c][(ka[i] >> shift) & 0xFF]++;
+                kb[pos] = ka[i];
+                vb[pos] = va[i];
+            }
         }
         uint64_t *tk = ka; ka = kb; kb = tk;
         uint32_t *tv = va; va = vb; vb = tv;
@@ -350,6 +378,7 @@ static int sort_pairs_u64(uint64_t *keys, uint32_t *vals, int64_t n, int end_bit
     }
     free(k2);
     free(v2);
+    free(cnt);
     return 0;
 }
 
@@ -360,24 +389,32 @@ int oracle_bin(const OracleIn *in, const float *depths, const int32_t *radii,
                uint32_t *vals, uint32_t *ranges) {
     const uint32_t gx = (uint32_t)((in->W + BLOCK_X - 1) / BLOCK_X);
     const uint32_t gy = (uint32_t)((in->H + BLOCK_Y - 1) / BLOCK_Y);
+    /* InclusiveSum(tiles_touched) as exclusive offsets, then duplicateWithKeys per Gaussian */
+    int64_t *offs = (int64_t *)malloc((size_t)(in->P > 0 ? in->P : 1) * sizeof(int64_t));
+    if (!offs) return -1;
     int64_t off = 0;
+    for (int64_t idx = 0; idx < in->P; ++idx) {
+        offs[idx] = off;
+        if (radii[idx] > 0) off += tiles_touched[idx];
+    }
+    if (off != K) { free(offs); return -3; }
+#pragma omp parallel for schedule(static, 4096)
     for (int64_t idx = 0; idx < in->P; ++idx) {
         if (radii[idx] > 0) {
             uint32_t rmin[2], rmax[2];
             get_rect(means2D[2 * idx], means2D[2 * idx + 1], radii[idx], gx, gy, rmin, rmax);
             uint32_t dbits;
             memcpy(&dbits, &depths[idx], 4);
+            int64_t o = offs[idx];
             for (uint32_t y = rmin[1]; y < rmax[1]; ++y)
                 for (uint32_t x = rmin[0]; x < rmax[0]; ++x) {
-                    if (off >= K) return -2;
-                    keys[off] = ((uint64_t)(y * gx + x) << 32) | dbits;
-                    vals[off] = (uint32_t)idx;
-                    ++off;
+                    keys[o] = ((uint64_t)(y * gx + x) << 32) | dbits;
+                    vals[o] = (uint32_t)idx;
+                    ++o;
                 }
         }
-        (void)tiles_touched;
     }
-    if (off != K) return -3;
+    free(offs);
     const int bit = (int)get_higher_msb(gx * gy);
     if (sort_pairs_u64(keys, vals, K, 32 + bit) != 0) return -1;
     memset(ranges, 0, (size_t)gx * gy * 2 * sizeof(uint32_t));
@@ -404,6 +441,7 @@ void oracle_render(const OracleIn *in, const uint32_t *ranges, const uint32_t *p
     const int W = in->W, H = in->H;
     const uint32_t gx = (uint32_t)((W + BLOCK_X - 1) / BLOCK_X);
     const uint32_t gy = (uint32_t)((H + BLOCK_Y - 1) / BLOCK_Y);
+#pragma omp parallel for collapse(2) schedule(dynamic, 4)
     for (uint32_t ty = 0; ty < gy; ++ty)
         for (uint32_t tx = 0; tx < gx; ++tx) {
             const uint32_t r0 = ranges[2 * (ty * gx + tx)], r1 = ranges[2 * (ty * gx + tx) + 1];
@@ -438,6 +476,15 @@ void oracle_render(const OracleIn *in, const uint32_t *ranges, const uint32_t *p
                         out_color[(size_t)ch * H * W + pid] = C[ch] + T * in->bg[ch];
                 }
         }
+}
+
+/* Threads of the parallel loops above (< 1: back to OpenMP's initial default, e.g.
+ * OMP_NUM_THREADS); returns the count in effect. */
+int oracle_set_threads(int n) {
+    static int initial = 0;
+    if (initial == 0) initial = omp_get_max_threads();
+    omp_set_num_threads(n >= 1 ? n : initial);
+    return omp_get_max_threads();
 }
 
 /* Reference sort backend (renderer_ogl.py:10-19): view-space z of every point.  The

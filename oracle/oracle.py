@@ -64,8 +64,16 @@ def lib() -> ctypes.CDLL:
         L.oracle_view_depth.argtypes = [vp, i64, vp, vp]
         L.oracle_argsort_f32.restype = ctypes.c_int
         L.oracle_argsort_f32.argtypes = [vp, i64, vp]
+        L.oracle_set_threads.restype = ctypes.c_int
+        L.oracle_set_threads.argtypes = [ctypes.c_int]
         _lib = L
     return _lib
+
+
+def set_threads(n: int) -> int:
+    """OpenMP threads of the oracle's parallel loops (n < 1: the default, OMP_NUM_THREADS or
+    the core count).  Results do not depend on it.  Returns the thread count in effect."""
+    return int(lib().oracle_set_threads(int(n)))
 
 
 def _c(a, dtype=np.float32):

@@ -14,6 +14,9 @@ Captured:
   camera.npz        -- util.Camera.get_project_matrix / get_htanfovxy_focal (util.py:82-113)
                        at the four benchmark resolutions.
   naive_gaussian.npz-- util_gau.naive_gaussian() (util_gau.py:25-60).
+  camera_data.npz   -- the 18 viewer poses of the reference's camera_data.csv (front, up,
+                       position per row; written by main.py:418-434, read by main.py:529-562),
+                       as float32 rows: data the reference ships, parsed with numpy.
   ply_ref.npz       -- util_gau.load_ply (util_gau.py:63-125) itself: its activations (:114-124),
                        f_rest reorder (:87-100), bounding box and center, on raw vertex arrays
                        stored in the same file.  plyfile is absent, so `PlyData.read` is a shim
@@ -117,7 +120,16 @@ def make_ply_ref(util_gau, tmpdir):
     np.savez_compressed(os.path.join(HERE, "ply_ref.npz"), **out)
 
 
+def make_camera_data():
+    rows = np.loadtxt(os.path.join(REF, "camera_data.csv"), delimiter=",", dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, "camera_data.npz"), rows=rows.astype(np.float32))
+    print(f"wrote camera_data.npz ({len(rows)} poses)")
+
+
 def main(only=None):
+    if only == "camera_data":
+        make_camera_data()
+        return
     _stub_modules()
     sys.path.insert(0, REF)
     import renderer_ogl  # noqa: E402  (the reference module)

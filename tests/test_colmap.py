@@ -146,3 +146,35 @@ def test_camera_markers():
     np.testing.assert_array_equal(xyz, [[1, 2, 3], [-1, 0.5, 0]])
     assert rot.shape == (2, 4) and scale.shape == (2, 3) and sh.shape == (2, 48)
     assert not op.any() and (scale == np.float32(0.03)).all()
+
+
+def test_reference_camera_data_csv_through_the_renderer(tmp_path, golden):
+    """The reference's own camera_data.csv (18 viewer poses, tests/golden/camera_data.npz): the
+    CSV reader returns every row, and HIPRenderer.update_camera_intrin / update_camera_pose
+    (renderer_cuda.py:181-203 on CPU tensors here) upload exactly the upstream settings of the
+    lookAt(pos, pos + front, up) view in the viewer's 1160x522 window."""
+    from gaussiansplattingviewer_amd.camera import cuda_camera_inputs, look_at
+    from gaussiansplattingviewer_amd.renderer import HIPRenderer
+    rows = golden("camera_data.npz")["rows"]
+    p = tmp_path / "camera_data.csv"
+    p.write_text("".join(",".join(repr(float(v)) for v in r) + "\n" for r in rows))
+    poses = colmap.read_camera_poses_from_csv(str(p))
+    assert len(poses) == len(rows) == 18
+    r = HIPRenderer(1160, 522, device="cpu")
+    for pose, row in zip(poses, rows):
+        np.testing.assert_array_equal(pose["camera_front"], row[0:3])
+        np.testing.assert_array_equal(pose["camera_position"], row[6:9])
+        cam = Camera(522, 1160)
+        r.update_camera_intrin(cam)
+        r.update_camera_pose(cam, True, pose)
+        view = look_at(row[6:9], row[6:9] + row[0:3], row[3:6])
+        cam_ref = Camera(522, 1160)
+        cam_ref.position = row[6:9]
+        want_view, want_proj, want_campos, tx, ty = cuda_camera_inputs(cam_ref, view)
+        rs = r.raster_settings
+        np.testing.assert_array_equal(rs["viewmatrix"].numpy(), want_view)
+        np.testing.assert_array_equal(rs["projmatrix"].numpy(), want_proj)
+        np.testing.assert_array_equal(rs["campos"].numpy(), want_campos)
+        assert (rs["tanfovx"], rs["tanfovy"]) == (tx, ty)
+        # the camera sits inside the synthetic cloud's cube for all but one pose
+        assert np.linalg.norm(row[6:9]) < 7.0

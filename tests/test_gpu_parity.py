@@ -2,7 +2,11 @@
 
 Bit-exact: radii, tiles_touched, depths, means2D, conic_opacity, rgb, num_rendered, the
 sorted point list, its tile ids, and the tile ranges.  Image (color, final_T, n_contrib): the
-tolerance in gpu_helpers.py (expf is the only non-bit-exact operation)."""
+tolerance in gpu_helpers.py -- the blend is the only stage that is not bit-exact (exp, and in
+the default fast arithmetic the fused multiply-adds of the staged quadratic; see there).  The
+viewer's own call requests no per-pixel extras, which selects the blend's paired-slot variant:
+every forward case is also rendered that way and must be bit-identical to the frame rendered
+with the extras."""
 import numpy as np
 import pytest
 import torch
@@ -57,6 +61,16 @@ def test_forward_parity(gpu, oracle_mod, name):
     hip = run_hip(s, gpu)
     assert orc["num_rendered"] > 0
     assert_parity(hip, orc)
+    _assert_plain_call_identical(gpu, s, hip)
+
+
+def _assert_plain_call_identical(gpu, s, hip):
+    """The viewer's call (no extras: the blend's n_contrib-free, paired-slot variant) renders the
+    same bits as the call with every extra output."""
+    plain = run_hip(s, gpu, extras=(), binning=False)
+    np.testing.assert_array_equal(plain["color"].view(np.uint32), hip["color"].view(np.uint32))
+    np.testing.assert_array_equal(plain["radii"], hip["radii"])
+    assert plain["num_rendered"] == hip["num_rendered"]
 
 
 def test_naive_scene_viewer_window(gpu, oracle_mod):
@@ -260,18 +274,14 @@ def test_headline_config_c3(gpu, c3_oracle, fast):
         _set_option(gpu, _lib.GSR_OPT_BLEND_FAST, 1)
     assert orc["num_rendered"] > 5_000_000
     assert_parity(hip, orc)
+    if fast:
+        _assert_plain_call_identical(gpu, s, hip)
 
 
 VARIANTS = {  # [(option, alternative value, default), ...]
     "per_pair": [(_lib.GSR_OPT_COLUMN_PAIRS, 0, 1)],
-    "unpacked": [(_lib.GSR_OPT_COLUMN_PAIRS, 0, 1), (_lib.GSR_OPT_PACKED_PAIRS, 0, 1)],
-    "unfused": [(_lib.GSR_OPT_FUSED_BINNING, 0, 1)],
-    "tile_shape0": [(_lib.GSR_OPT_TILE_SORT_SHAPE, 0, 3)],
-    "tile_shape5": [(_lib.GSR_OPT_TILE_SORT_SHAPE, 5, 3)],
     "no_cull": [(_lib.GSR_OPT_BLEND_CULL, 0, 1)],
     "compact_sort": [(_lib.GSR_OPT_COMPACT_SORT, 1, -1)],
-    "inline_color": [(_lib.GSR_OPT_SPLIT_COLOR, 0, 1)],
-    "inline_color_unfused": [(_lib.GSR_OPT_SPLIT_COLOR, 0, 1), (_lib.GSR_OPT_FUSED_BINNING, 0, 1)],
 }
 
 
@@ -293,11 +303,10 @@ class _options:
 @pytest.mark.parametrize("variant", list(VARIANTS))
 @pytest.mark.parametrize("size", [(1920, 1080), (16, 16), (4200, 64)])
 def test_sort_implementations_agree(gpu, variant, size):
-    """The defaults (duplicate fused with the first reduce-then-scan pass, 8x8 sort tiles, the
-    blend's quadrant cull, colour on the second stream) and the alternatives -- separate
-    duplicate kernel, other sort tile shapes, no cull, inline colour -- give identical binning
-    and images.  Sizes: 1 tile (tbits = 0) and > 8 bits of
-    tile id in x."""
+    """The defaults (column-first binning, the blend's quadrant cull, the depth sort dropping
+    the off-strip keys in its first pass) and the alternatives -- the per-pair binning form, no
+    cull, a compacting depth sort -- give identical binning and images.  Sizes: 1 tile
+    (tbits = 0) and > 256 tile columns (the per-pair form either way)."""
     w, h = size
     P = 300_000 if w * h > 10_000 else 20_000
     s = scene_inputs(synthetic_gaussians(P, 3, 21), static_camera(w, h, (0.5, 0.2, 3.5)), 3)
@@ -309,7 +318,7 @@ def test_sort_implementations_agree(gpu, variant, size):
         np.testing.assert_array_equal(alt[k], ref[k], err_msg=k)
 
 
-@pytest.mark.parametrize("variant", ["default", "per_pair", "unpacked", "unfused", "compact_sort"])
+@pytest.mark.parametrize("variant", ["default", "per_pair", "compact_sort"])
 def test_long_tile_lists_and_depth_ties(gpu, oracle_mod, variant):
     """Tiles covered by more than 2048 splats (multi-chunk digit runs in the tile sort, long
     blend lists) and half of the Gaussians at one depth (ties: upstream orders them by
@@ -356,3 +365,29 @@ def test_tile_lists_of_one_depth(gpu, oracle_mod):
     g.xyz[:, 2] = np.float32(-0.5)
     s = scene_inputs(g, static_camera(160, 120, (0, 0, 3.0)), 1)
     assert_parity(run_hip(s, gpu), run_oracle(oracle_mod, s))
+
+
+def test_compacted_strip_colour_path(gpu):
+    """Compacted strip frames (GSR_OPT_COMPACT_SORT: auto on strips of >= 4M Gaussians, forced
+    here) colour only the compacted kept ids (k_color_ids, handed from the main stream's
+    compaction to the second stream by an event) when no rgb output is requested -- the bench's
+    and the viewer's call.  Every strip must be bit-identical to the same rows of the full frame
+    rendered without compaction (k_color over every Gaussian)."""
+    from gaussiansplattingviewer_amd.strips import strip_pixel_rows, strip_rows
+    W, H = 1920, 1080
+    s = scene_inputs(synthetic_gaussians(300_000, 3, 26), static_camera(W, H, (0.3, 0.2, 3.8)), 3)
+    pix = ("final_T", "n_contrib")  # no "rgb": the compacted-id colour pass is allowed
+    full = run_hip(s, gpu, extras=pix)
+    gy = (H + 15) // 16
+    _set_option(gpu, _lib.GSR_OPT_COMPACT_SORT, 1)
+    try:
+        for r in range(8):
+            rows = strip_rows(gy, 8, r)
+            part = run_hip(s, gpu, tile_rows=rows, extras=pix)
+            y0, n = strip_pixel_rows(rows, H)
+            for k, v in (("color", full["color"][:, y0:y0 + n]), ("final_T", full["final_T"][y0:y0 + n]),
+                         ("n_contrib", full["n_contrib"][y0:y0 + n])):
+                np.testing.assert_array_equal(part[k].view(np.uint32), v.view(np.uint32), err_msg=k)
+            np.testing.assert_array_equal(part["radii"], full["radii"])
+    finally:
+        _set_option(gpu, _lib.GSR_OPT_COMPACT_SORT, -1)

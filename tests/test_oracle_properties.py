@@ -85,3 +85,22 @@ def test_stable_argsort_matches_numpy(oracle_mod, n, seed, kind):
     else:
         d = (rng.normal(0, 1, n) * 1e30).astype(np.float32)
     np.testing.assert_array_equal(oracle_mod.argsort_stable(d), np.argsort(d, kind="stable"))
+
+
+def test_oracle_threads_do_not_change_results(oracle_mod):
+    """The oracle's OpenMP loops (bench.py's host-cores CPU baseline) give bit-identical results
+    at 1 and at 8 threads."""
+    g, view, proj, campos, tx, ty = _scene(120_000, 3, 400, 300, (0.4, -0.2, 3.5), 10.0, 0.25)
+    out = []
+    for n in (1, 8):
+        oracle_mod.set_threads(n)
+        out.append(oracle_mod.forward(g.xyz, g.opacity, view, proj, campos, tx, ty, 400, 300,
+                                      shs=g.sh, sh_degree=3, scales=g.scale, rotations=g.rot))
+    oracle_mod.set_threads(0)
+    a, b = out
+    assert a["num_rendered"] > 100_000
+    for k, v in a.items():
+        if isinstance(v, np.ndarray):
+            np.testing.assert_array_equal(np.asarray(b[k]).view(np.uint8), v.view(np.uint8), err_msg=k)
+        else:
+            assert b[k] == v, k

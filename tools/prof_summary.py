@@ -5,7 +5,8 @@ FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE counts exactly half of
 a wide coalesced streaming read (MI355X_MICROARCH.md §HBM), so the table shows the raw read
 bytes and the x2-corrected read bytes; WRITE_SIZE is exact for 16-B streaming stores.
 
-Usage: python tools/prof_summary.py gpurun_out/prof_<tag> [--out profiles/<name>.md]
+Usage: python tools/prof_summary.py gpurun_out/prof_<tag>_<config> [--out profiles/<name>.md]
+                                    [--json profiles/<tag>_<config>_kernels.json]
 """
 from __future__ import annotations
 
@@ -91,7 +92,9 @@ def main():
                       "read_bytes_x2": 2 * sum(f) / len(f) * 1024 if f else None,
                       "write_bytes": sum(w) / len(w) * 1024 if w else None}
         os.makedirs(os.path.dirname(a.json) or ".", exist_ok=True)
-        json.dump(out, open(a.json, "w"), indent=1, sort_keys=True)
+        sha = os.path.join(a.dir, "lib.sha")
+        json.dump({"source": a.dir, "lib_sha16": open(sha).read().strip() if os.path.exists(sha) else None,
+                   "kernels": out}, open(a.json, "w"), indent=1, sort_keys=True)
     print(text)
     if a.out:
         os.makedirs(os.path.dirname(a.out), exist_ok=True)

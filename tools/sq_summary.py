@@ -3,9 +3,10 @@ wave time spent issuing, waiting on dependencies / issue, and waiting on s_waitc
 SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles (MI355X_MICROARCH.md);
 GRBM_GUI_ACTIVE is summed over the 8 XCDs.
 
-Usage: python tools/sq_summary.py gpurun_out/pmc_<tag> [kernel-substring] [--json out.json]
---json writes the per-launch averages of every counter (keyed by the kernel substring), which
-bench.py reads for the blend's VALU roofline."""
+Usage: python tools/sq_summary.py gpurun_out/prof_<tag>_<config> [kernel-substring] [--json out.json]
+--json writes the per-launch averages of every counter (keyed by the kernel substring) and the
+profiled library's sha (lib.sha, tools/profile_config.sh), which bench.py matches against the
+library it loads for the blend's VALU roofline."""
 import collections
 import csv
 import glob
@@ -19,7 +20,7 @@ if out_json in args:
     args.remove(out_json)
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 names = set()
-for f in glob.glob(d + "/p*/**/pmc_counter_collection.csv", recursive=True):
+for f in glob.glob(d + "/p[0-9]*/**/pmc_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         if kern in r["Kernel_Name"]:
             names.add(r["Kernel_Name"].split("(")[0])
@@ -43,6 +44,9 @@ if "SQ_ACTIVE_INST_VALU" in res:
     # the known count of a calibration kernel; profiles/r02_valu_calibration.md)
     print(f"  SQ_ACTIVE_INST_VALU {res['SQ_ACTIVE_INST_VALU'] / 1e6:.1f} M (= VALU instructions)")
 if out_json:
+    import os
+    sha = os.path.join(d, "lib.sha")
     json.dump({"kernel": kern, "kernels_matched": sorted(names), "source": d,
+               "lib_sha16": open(sha).read().strip() if os.path.exists(sha) else None,
                "launches": launches, "per_launch": res}, open(out_json, "w"), indent=1)
     print("wrote", out_json)
