@@ -458,6 +458,7 @@ def main():
     # what the committed serial rocprofv3 trace reports for it; the timed region's blend events
     # (two frames in flight, the other frame's kernels sharing the CUs) are reported beside it.
     dom_ms = stage_ms["blend"]
+    default_opts = args.blend == "fast"  # the committed profiles are of the default arithmetic
     roofline = blend_roofline(args.config if default_opts else None, dom_ms, blend_ms_timed,
                               alg["blend"])
     roofline["frame_alg_gbs"] = round(sum(alg.values()) / (t_max / args.steps) / 1e9, 2)

@@ -64,7 +64,8 @@ def test_reference_viewer_pose(gpu, oracle_mod, viewer, i):
                              rs["tanfovy"], W, H, shs=host(g.sh).reshape(len(radii), -1),
                              sh_degree=rs["sh_degree"], scales=host(g.scale),
                              rotations=host(g.rot), bg=host(rs["bg"]))
-    assert orc["num_rendered"] > 0
+    # every pose sees part of the scene except the last, saved 6.8 units out, looking away
+    assert (orc["num_rendered"] > 0) == (i != 17)
     assert len(pl) == orc["num_rendered"]
     np.testing.assert_array_equal(radii, orc["radii"])
     np.testing.assert_array_equal(pl.cpu().numpy().view(np.uint32), orc["point_list"])
