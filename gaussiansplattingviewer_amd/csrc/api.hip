@@ -618,7 +618,7 @@ int forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings 
     // D (the bits in which the kept depth keys differ) arrives in pinned memory from pass 0's
     // scan, tagged with this frame, while pass 0's downsweep runs: the host then queues only the
     // passes D needs.  Without it every pass is queued and the unneeded ones exit at once.
-    int depth_passes = 3;
+    int depth_passes = gsr_depth_sort_passes(32);  // all
     uint64_t dv = 0;
     if (ctx->last_K >= kWaitDPairs &&
         spin_on(&ctx->h_total[4], [&](uint64_t v) { return (uint32_t)(v >> 32) == f.tag; }, dv))
@@ -892,7 +892,7 @@ int gsr_depth_argsort(gsr_context *ctx, const float *xyz, int64_t P, const float
                            static_cast<uint2 *>(ctx->ds_b.p), reinterpret_cast<uint32_t *>(out_index),
                            static_cast<uint32_t *>(ctx->hist.p),
                            static_cast<uint32_t *>(ctx->digit_total.p),
-                           static_cast<uint32_t *>(ctx->ds_ctl.p), 0, 3, s),
+                           static_cast<uint32_t *>(ctx->ds_ctl.p), 0, gsr_depth_sort_passes(32), s),
             "depth argsort launch");
     return GSR_OK;
 }

@@ -325,7 +325,8 @@ hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_firs
                                     uint32_t *digit_total, uint32_t *keys_out, uint32_t *vals_out,
                                     uint2 *ranges_zero, uint32_t n_ranges, hipStream_t s);
 // Column-first pair generation (binning.hip): pass 1 of the tile sort on (Gaussian, column)
-// segments of the depth-sorted Gaussians.  hist: gsr_col_blocks(n_max) * 256 words.
+// segments of the depth-sorted Gaussians.  hist: gsr_col_blocks(n_max) * 256 words (per group of
+// 4 blocks its column totals, per block its offsets within the group).
 int64_t gsr_col_blocks(int64_t n);
 hipError_t gsr_launch_col_pairs_count(const uint32_t *perm, const uint2 *strip_rect, int64_t n_max,
                                       const uint32_t *d_n, uint2 *rect_sorted, uint32_t *hist,

@@ -322,10 +322,24 @@ __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__
     __shared__ uint32_t s_or[16], s_and[16];
     unsigned long long v = 0;
     uint32_t o = 0u, a = 0xFFFFFFFFu;
-    for (int64_t i = threadIdx.x; i < n; i += 1024) {
-        v += cnt[i];
-        o |= keybits[i].x;
-        a &= keybits[i].y;
+    // 8 blocks' entries per thread and round, their loads in flight together (one dependent
+    // load per 1024 blocks took 23 us at 6M Gaussians)
+    constexpr int kU = 8;
+    for (int64_t i0 = threadIdx.x; i0 < n; i0 += kU * 1024) {
+        unsigned long long c[kU];
+        uint2 kb[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t i = i0 + (int64_t)u * 1024;
+            c[u] = i < n ? cnt[i] : 0ull;
+            kb[u] = i < n ? keybits[i] : make_uint2(0u, 0xFFFFFFFFu);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            v += c[u];
+            o |= kb[u].x;
+            a &= kb[u].y;
+        }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
