@@ -139,12 +139,21 @@ def check(rc: int, what: str) -> int:
     return rc
 
 
+def _native_shares_library() -> bool:
+    """The `_native` extension links the in-tree libgsr.so; contexts are shared with it only
+    when this module loaded that same file (not a GSR_LIB A/B build)."""
+    default = os.path.join(_HERE, "libgsr.so")
+    return os.path.exists(LIB_PATH) and os.path.samefile(LIB_PATH, default)
+
+
 def context(device_index: int, slot: int = 0) -> ctypes.c_void_p:
     """The process-wide gsr_context of a device (created on first use, on that device).
 
     `slot` selects one of several independent contexts per device (own workspace, own
     second stream): frames rendered through different slots on different streams may be in
-    flight at the same time (`pipeline.FramePipeline`)."""
+    flight at the same time (`pipeline.FramePipeline`).  Slot 0 is the context the `_C`
+    extension (`_native.so`) renders with, so the upstream entry points and this module share
+    one workspace and `binning_state()` sees a `GaussianRasterizer` forward."""
     import torch
 
     lib = load_library()
@@ -156,23 +165,32 @@ def context(device_index: int, slot: int = 0) -> ctypes.c_void_p:
         if not torch.cuda.is_available():
             raise RuntimeError("gaussiansplattingviewer_amd needs a HIP device (MI355X); "
                                "torch.cuda.is_available() is False")
-        with torch.cuda.device(device_index):
-            ctx = ctypes.c_void_p()
-            check(lib.gsr_create(ctypes.byref(ctx)), "gsr_create")
+        if key[1] == 0 and _native_shares_library():
+            from . import _native  # owns (creates and destroys) the slot-0 contexts
+            ctx = ctypes.c_void_p(_native.context_handle(key[0]))
+        else:
+            with torch.cuda.device(device_index):
+                ctx = ctypes.c_void_p()
+                check(lib.gsr_create(ctypes.byref(ctx)), "gsr_create")
         _contexts[key] = ctx
         return ctx
 
 
 def release_contexts() -> None:
     """Destroy every gsr_context (registered with atexit; a diagnostics build reports its
-    counters from gsr_destroy)."""
+    counters from gsr_destroy); slot 0's belong to `_native`."""
     with _lock:
         lib = _lib
         if lib is None or not _contexts:
             return
-        for ctx in _contexts.values():
-            lib.gsr_destroy(ctx)
+        native = _native_shares_library() and any(slot == 0 for _, slot in _contexts)
+        for (_, slot), ctx in _contexts.items():
+            if slot != 0 or not native:
+                lib.gsr_destroy(ctx)
         _contexts.clear()
+        if native:
+            from . import _native
+            _native.release_contexts()
 
 
 atexit.register(release_contexts)

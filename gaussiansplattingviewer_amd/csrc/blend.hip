@@ -18,6 +18,8 @@
 // (5 FMA per pixel, then the raw v_exp_f32); 0 keeps upstream's per-pixel operation order (the
 // core of ocml's expf).  Both are within the
 // image tolerance of tests/gpu_helpers.py.
+#include <type_traits>
+
 #include "gsr_internal.h"
 
 using namespace gsr;
@@ -125,31 +127,37 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
     auto live_any = [&]() { return __ballot(!(T <= 0.0f)) != 0ull; };
     if (!live_any()) return;
 
-    auto composite = [&](const StagedSplat &sp) {
+    // kBound (fast form): test upstream's power > 0 skip as p > bound -- only chunks holding a
+    // conic that is not positive definite need it (staging below)
+    auto composite = [&](const StagedSplat &sp, auto bound_tag) {
+        constexpr bool kBound = decltype(bound_tag)::value;
         bool vis, acc, term;
         float test_T;
         if (kFast) {
             // The loop-carried chain is only T -> T (1 - alpha_eff) -> compare -> select:
-            // alpha_eff = 0 for an invisible splat (then test_T = T and the weight T - test_T
-            // is 0), and a pixel that terminates keeps -|T| (idempotent once done).
+            // alpha_eff = 0 for an invisible splat (then test_T = T), and a pixel that
+            // terminates keeps -|T| (idempotent once done).  The weight is |T| - |T'|: T - test_T
+            // while the pixel composites, 0 for the terminating splat and after it.
             float p2 = __builtin_fmaf(sp.g.y, pu, sp.g.x);
             p2 = __builtin_fmaf(sp.g.z, pv, p2);
             p2 = __builtin_fmaf(sp.g.w, puu, p2);
             p2 = __builtin_fmaf(sp.q.x, puv, p2);
             p2 = __builtin_fmaf(sp.q.y, pvv, p2);
             const float alpha = fminf(0.99f, __builtin_amdgcn_exp2f(p2));
-            vis = !(p2 > sp.e.z) && !(alpha < 1.0f / 255.0f);
+            vis = !(alpha < 1.0f / 255.0f);
+            if (kBound) vis = vis && !(p2 > sp.e.z);
             // T (1 - alpha) as one fma, T - alpha T; alpha_eff = 0 leaves T exactly
             const float alpha_eff = vis ? alpha : 0.0f;
             test_T = __builtin_fmaf(-T, alpha_eff, T);
             const bool lo = test_T < 0.0001f;
-            const float wgt = lo ? 0.0f : T - test_T;
+            const float T_next = lo ? -fabsf(T) : test_T;
+            const float wgt = fabsf(T) - fabsf(T_next);
             C0 = __builtin_fmaf(sp.q.z, wgt, C0);
             C1 = __builtin_fmaf(sp.q.w, wgt, C1);
             C2 = __builtin_fmaf(sp.e.x, wgt, C2);
             if (kContrib)
                 last_contributor = (vis && !lo) ? __float_as_uint(sp.e.y) : last_contributor;
-            T = lo ? -fabsf(T) : test_T;
+            T = T_next;
             return;
         } else {
             const float dx = sp.g.x - pfx, dy = sp.g.y - pfy;
@@ -184,6 +192,7 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
             keep = may_touch(r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.z, r.b.w, 2.0f * r.c.x, X0,
                              X0 + 7, Y0, Y0 + 7);
         const uint64_t bal = __ballot(keep);
+        bool npd = false;  // a staged conic that is not positive definite (fast form)
         if (keep) {
             StagedSplat st;
             if (kFast) {
@@ -202,6 +211,7 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
                 // rounding; the expanded form rounds differently (at a centre that falls on a
                 // pixel it can land just above 0), so the test is kept for the other conics only
                 const bool pd = ca < 0.0f && cc < 0.0f && 4.0f * ca * cc > cb * cb;
+                npd = !pd;
                 st.e = make_float4(r.c.w, __uint_as_float(idx - range.x + 1u),
                                    pd ? __builtin_huge_valf() : lo, 0.0f);
             } else {
@@ -227,15 +237,17 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
         if (count == 0) continue;
         // the compacted slots are the list (no index indirection); an odd count is padded with
         // an opacity-0 splat in slot `count` (< 64 for an odd count): exact: opacity 0; fast:
-        // exponent 0 against a power bound of -inf (never visible)
+        // exponent -inf (alpha 0, the bound-free loop included) and a power bound of -inf
         if (count & 1) {
             if (kPair) {
-                if (lane < 8) reinterpret_cast<float *>(&s_spl[count])[lane] = 0.0f;
+                if (lane < 8)
+                    reinterpret_cast<float *>(&s_spl[count])[lane] =
+                        lane == 0 ? -__builtin_huge_valf() : 0.0f;
                 if (lane == 8) s_spl[count - 1].e.y = 0.0f;
                 if (lane == 9) s_spl[count - 1].e.w = -__builtin_huge_valf();
             } else if (lane < 12) {
                 reinterpret_cast<float *>(&s_spl[count])[lane] =
-                    (kFast && lane == 10) ? -__builtin_huge_valf() : 0.0f;
+                    (kFast && (lane == 0 || lane == 10)) ? -__builtin_huge_valf() : 0.0f;
             }
             ++count;
         }
@@ -243,18 +255,27 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
 
         // single-buffered: a software-pipelined form (the next pair's LDS reads in flight
         // during this pair) spilled past 64 VGPRs and was slower
-        for (int k = 0; k < count; k += 2) {
-            if (kPair) {
-                const float4 e = s_spl[k].e;
-                composite(StagedSplat{s_spl[k].g, s_spl[k].q, make_float4(e.x, 0.0f, e.z, 0.0f)});
-                composite(
-                    StagedSplat{s_spl[k + 1].g, s_spl[k + 1].q, make_float4(e.y, 0.0f, e.w, 0.0f)});
-            } else {
-                const StagedSplat a0 = s_spl[k], a1 = s_spl[k + 1];
-                composite(a0);
-                composite(a1);
+        auto composite_all = [&](auto bound_tag) {
+            for (int k = 0; k < count; k += 2) {
+                if (kPair) {
+                    const float4 e = s_spl[k].e;
+                    composite(StagedSplat{s_spl[k].g, s_spl[k].q, make_float4(e.x, 0.0f, e.z, 0.0f)},
+                              bound_tag);
+                    composite(StagedSplat{s_spl[k + 1].g, s_spl[k + 1].q,
+                                          make_float4(e.y, 0.0f, e.w, 0.0f)},
+                              bound_tag);
+                } else {
+                    const StagedSplat a0 = s_spl[k], a1 = s_spl[k + 1];
+                    composite(a0, bound_tag);
+                    composite(a1, bound_tag);
+                }
             }
-        }
+        };
+        // (the exact form always tests power > 0, as upstream writes it)
+        if (!kFast || __ballot(npd) != 0ull)
+            composite_all(std::integral_constant<bool, true>{});
+        else
+            composite_all(std::integral_constant<bool, false>{});
         if (!live_any()) break;
     }
 

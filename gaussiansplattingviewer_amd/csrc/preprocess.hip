@@ -166,26 +166,30 @@ __device__ __forceinline__ float3 eval_sh3_stream(float3 pos, const float *campo
 // alpha >= 1/255 is  q(d) = A dx^2 + 2B dx dy + C dy^2 <= 2 L,  L = ln(255 o)  (upstream
 // alpha = min(0.99, o exp(power)), power = -q/2).  Returns {ex, ey, Lm}: Lm >= L widened by an
 // absolute bound on the float rounding of the blend's `power` inside the box plus margins, and
-// the half-extents (pixels) of the ellipse q <= 2 Lm.  Computed in double from the float conic
-// the blend evaluates.  Used only to skip (splat, 8x8 quadrant) pairs that provably cannot
-// contribute; outputs are identical with and without it (tested).
+// the half-extents (pixels) of the ellipse q <= 2 Lm, from the float conic the blend evaluates.
+// Used only to skip (splat, 8x8 quadrant) pairs that provably cannot contribute; outputs are
+// identical with and without it (tested).  The determinant is formed in double (A C ~ B^2 for
+// elongated splats would cancel in float); the rest is float, whose rounding (~1e-6 relative
+// over the chain) sits far inside the margins (+1e-3 and x1.01 on L, +0.02 px on the extents).
+// (An all-double version spent ~1/3 of the preprocess kernel's VALU on software log / div.)
 __device__ __forceinline__ float3 cull_data(float A, float B, float C, float o) {
     const float kInf = __builtin_huge_valf();
-    const double det = (double)A * (double)C - (double)B * (double)B;
-    if (!(det > 0.0) || !(A > 0.0f) || !(C > 0.0f) || !(o == o))
+    const double det_d = (double)A * (double)C - (double)B * (double)B;
+    if (!(det_d > 0.0) || !(A > 0.0f) || !(C > 0.0f) || !(o == o))
         return make_float3(kInf, kInf, kInf);
-    double L = log(255.0 * (double)o);
-    if (L < 0.0) L = 0.0;
-    const double sxx = (double)C / det, syy = (double)A / det;  // inverse of the conic
-    double ex = sqrt(2.0 * L * sxx), ey = sqrt(2.0 * L * syy);
+    const float det = (float)det_d;  // > 0, or 0 / denormal -> infinite extents below
+    float L = __logf(255.0f * o);
+    if (!(L > 0.0f)) L = 0.0f;
+    const float sxx = C / det, syy = A / det;  // inverse of the conic
+    float ex = sqrtf(2.0f * L * sxx), ey = sqrtf(2.0f * L * syy);
     // |float(power) - power| <= ~8 eps (|A|dx^2 + |C|dy^2 + 2|B dx dy|) inside the box.
-    const double mag = ((double)A + (double)C + 2.0 * fabs((double)B)) * (ex * ex + ey * ey);
-    const double Lm = (L + 8.0 * 5.96e-8 * mag + 1e-3) * 1.01;
-    ex = sqrt(2.0 * Lm * sxx) + 0.02;
-    ey = sqrt(2.0 * Lm * syy) + 0.02;
-    if (!(ex < 1e30) || !(ey < 1e30) || !(Lm < 1e30)) return make_float3(kInf, kInf, kInf);
-    // round Lm up: one ulp above its float conversion (Lm > 0 and finite here)
-    return make_float3((float)ex, (float)ey, __uint_as_float(__float_as_uint((float)Lm) + 1u));
+    const float mag = (A + C + 2.0f * fabsf(B)) * (ex * ex + ey * ey);
+    const float Lm = (L + 8.0f * 5.96e-8f * mag + 1e-3f) * 1.01f;
+    ex = sqrtf(2.0f * Lm * sxx) + 0.02f;
+    ey = sqrtf(2.0f * Lm * syy) + 0.02f;
+    if (!(ex < 1e30f) || !(ey < 1e30f) || !(Lm < 1e30f)) return make_float3(kInf, kInf, kInf);
+    // round Lm up by one ulp (Lm > 0 and finite here)
+    return make_float3(ex, ey, __uint_as_float(__float_as_uint(Lm) + 1u));
 }
 
 // Returns the number of (Gaussian, strip tile) pairs of Gaussian idx.

@@ -183,10 +183,12 @@ class _RasterizeGaussians(torch.autograd.Function):
         from . import _C
         del means2D  # only carries screen-space gradients upstream
         rs = raster_settings
-        args = (rs.bg, means3D, colors_precomp, opacities, scales, rotations, rs.scale_modifier,
-                cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy,
-                rs.image_height, rs.image_width, sh, rs.sh_degree, rs.campos, rs.prefiltered,
-                rs.debug)
+        # absent inputs travel as empty tensors, as upstream's __init__.py passes them
+        none = lambda t: torch.empty(0) if t is None else t  # noqa: E731
+        args = (rs.bg, means3D, none(colors_precomp), opacities, none(scales), none(rotations),
+                rs.scale_modifier, none(cov3Ds_precomp), rs.viewmatrix, rs.projmatrix,
+                rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, none(sh), rs.sh_degree,
+                rs.campos, rs.prefiltered, rs.debug)
         num_rendered, color, radii, geom, binning, img = _C.rasterize_gaussians(*args)
         ctx.num_rendered = num_rendered
         ctx.mark_non_differentiable(radii)
@@ -204,26 +206,12 @@ class GaussianRasterizer(torch.nn.Module):
         self.raster_settings = raster_settings
 
     def markVisible(self, positions: torch.Tensor) -> torch.Tensor:
-        """Frustum-cull test per point: view-space z > 0.2 (upstream markVisible)."""
+        """Frustum-cull test per point: view-space z > 0.2 (upstream markVisible, through
+        `_C.mark_visible`)."""
+        from . import _C
         with torch.no_grad():
             rs = self.raster_settings
-            device = _device_of(positions)
-            positions = _as_dev(positions, device, "P,3")
-            P = int(positions.size(0)) if positions is not None else 0
-            visible = torch.zeros((P,), dtype=torch.bool, device=device)
-            if P == 0:
-                return visible
-            view = _as_dev(rs.viewmatrix, device, "4,4")
-            proj = _as_dev(rs.projmatrix, device, "4,4")
-            idx = device.index if device.index is not None else torch.cuda.current_device()
-            lib = _lib.load_library()
-            with torch.cuda.device(idx):
-                _lib.check(lib.gsr_mark_visible(
-                    _lib.context(idx), positions.data_ptr(), P, view.data_ptr(),
-                    proj.data_ptr(), visible.data_ptr(),
-                    ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)),
-                    "gsr_mark_visible")
-            return visible
+            return _C.mark_visible(positions, rs.viewmatrix, rs.projmatrix)
 
     def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None,
                 rotations=None, cov3D_precomp=None):

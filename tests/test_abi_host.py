@@ -125,41 +125,57 @@ def test_strip_rows_partition(gy, world):
     assert covered == H
 
 
-def test_native_entry_returns_upstream_6_tuple(monkeypatch):
-    """`_C.rasterize_gaussians` has upstream's argument order and 6-field return
-    (num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer), and GaussianRasterizer
-    reaches it through `_RasterizeGaussians` (upstream __init__.py's call chain).  The native
-    call itself is replaced here (no GPU in the CPU suite); the GPU suite runs the real one."""
-    from gaussiansplattingviewer_amd import _C, rasterizer
+def test_torch_extension_binds_upstream_entry_points():
+    """`_C` is the compiled PyTorch extension (_native.so, csrc/torch_ext.cpp) over libgsr.so:
+    upstream's two entry points with their argument counts, the same ABI as the ctypes
+    loader, and upstream's input checks (these fail before any device call)."""
+    from gaussiansplattingviewer_amd import _C, _native
+    assert _C.rasterize_gaussians is _native.rasterize_gaussians
+    assert _C.mark_visible is _native.mark_visible
+    assert _native.__file__.endswith("_native.so")
+    assert _native.abi_version() == _lib.load_library().gsr_abi_version() == _lib.ABI_VERSION
+    sig = _native.rasterize_gaussians.__doc__.splitlines()[0]
+    assert sig.startswith("rasterize_gaussians(") and sig.count("arg") == 19, sig
+    assert _native.mark_visible.__doc__.splitlines()[0].count("arg") == 3
+    e = torch.empty(0)
+    with pytest.raises(RuntimeError, match=r"means3D must have dimensions \(num_points, 3\)"):
+        _C.rasterize_gaussians(torch.zeros(3), torch.zeros(4, 4), e, torch.ones(4, 1), e, e, 1.0,
+                               e, torch.eye(4), torch.eye(4), 0.5, 0.5, 8, 8, e, 0,
+                               torch.zeros(3), False, False)
+    with pytest.raises(RuntimeError, match="must be a device"):
+        _C.rasterize_gaussians(torch.zeros(3), torch.zeros(4, 3), e, torch.ones(4, 1), e, e, 1.0,
+                               e, torch.eye(4), torch.eye(4), 0.5, 0.5, 8, 8, e, 0,
+                               torch.zeros(3), False, False)
+    with pytest.raises(RuntimeError, match="must be a device"):
+        _C.mark_visible(torch.zeros(4, 3), torch.eye(4), torch.eye(4))
+
+
+def test_rasterizer_reaches_native_entry_with_upstream_args(monkeypatch):
+    """GaussianRasterizer reaches `_C.rasterize_gaussians` through `_RasterizeGaussians`
+    (upstream __init__.py's call chain) with upstream's argument order, absent inputs as empty
+    tensors, and keeps (color, radii) of the 6-field return.  The native call is replaced here
+    (no GPU in the CPU suite); the GPU suite runs the real one."""
+    from gaussiansplattingviewer_amd import _C
     seen = {}
 
-    def fake_native(*args, **kw):
+    def fake_native(*args):
         seen["args"] = args
         P = args[1].shape[0]
         H, W = args[12], args[13]
-        return rasterizer.ForwardResult(7, torch.zeros(3, H, W), torch.ones(P, dtype=torch.int32),
-                                        {})
+        u8 = torch.empty(0, dtype=torch.uint8)
+        return 7, torch.zeros(3, H, W), torch.ones(P, dtype=torch.int32), u8, u8, u8
 
-    monkeypatch.setattr(_C, "rasterize_gaussians_native", fake_native)
+    monkeypatch.setattr(_C, "rasterize_gaussians", fake_native)
     P, H, W = 5, 4, 6
     xyz, op = torch.zeros(P, 3), torch.ones(P, 1)
     sc, rot, sh = torch.ones(P, 3), torch.ones(P, 4), torch.zeros(P, 16, 3)
-    out = _C.rasterize_gaussians(torch.zeros(3), xyz, None, op, sc, rot, 1.0, None,
-                                 torch.eye(4), torch.eye(4), 0.5, 0.4, H, W, sh, 3,
-                                 torch.zeros(3), False, False)
-    assert len(out) == 6
-    num_rendered, color, radii, geom, binning, img = out
-    assert isinstance(num_rendered, int) and num_rendered == 7
-    assert tuple(color.shape) == (3, H, W) and color.dtype == torch.float32
-    assert tuple(radii.shape) == (P,) and radii.dtype == torch.int32
-    for b in (geom, binning, img):
-        assert isinstance(b, torch.Tensor) and b.dtype == torch.uint8
-    assert seen["args"][12:16] == (H, W, sh, 3)  # image_height, image_width, sh, sh_degree
-
     rs = GaussianRasterizationSettings(H, W, 0.5, 0.4, torch.zeros(3), 1.0, torch.eye(4),
                                        torch.eye(4), 3, torch.zeros(3), False, False)
-    seen.clear()
     c2, r2 = GaussianRasterizer(rs)(means3D=xyz, means2D=None, opacities=op, shs=sh,
                                     colors_precomp=None, scales=sc, rotations=rot,
                                     cov3D_precomp=None)
-    assert seen["args"][1] is xyz and tuple(c2.shape) == (3, H, W)
+    a = seen["args"]
+    assert len(a) == 19 and a[1] is xyz and a[3] is op and a[4] is sc and a[5] is rot
+    assert a[14] is sh and a[12:14] == (H, W) and a[15] == 3
+    assert a[2].numel() == 0 and a[7].numel() == 0  # colors_precomp, cov3D_precomp absent
+    assert tuple(c2.shape) == (3, H, W) and tuple(r2.shape) == (P,)
