@@ -91,6 +91,7 @@ struct gsr_context {
     DevBuf tile_keys, tile_vals, tile_keys_alt, tile_vals_alt;
     DevBuf ranges_local;
     DevBuf tile_diff;  // difference-array partials of the second-stream tile ranges
+    DevBuf blend_order;  // the blend's tile groups, heaviest first (second stream)
     // pinned host words the GPU stores into: [0] -, [1] -, [2] K (k_publish_K), [3] its depth-key
     // bits, [4] (frame tag << 32) | D from the depth sort's pass 0, [5] -, [6] -, [7] K's tag
     uint64_t *h_total = nullptr;
@@ -108,6 +109,10 @@ struct gsr_context {
     int cull = 1;
     int fast = 1;
     int column_pairs = 1;
+#ifndef GSR_BLEND_ORDER_DEFAULT
+#define GSR_BLEND_ORDER_DEFAULT 1
+#endif
+    int blend_order_on = GSR_BLEND_ORDER_DEFAULT;  // (lab A/B builds set it to 0)
     int compact_sort = -1;
     // stage timing: a ring of event sets, one per timed forward, read back after the timed region
     int timing = 0;        // 0 off, 1 every stage, 2 the blend only, on every 8th forward
@@ -305,9 +310,12 @@ int setup_frame(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
 
     GSR_TRY(reserve_P(ctx, P, s));
     GSR_TRY(grow(ctx, ctx->ranges_local, (size_t)std::max<uint64_t>(f.T_strip, 1) * 8, s));
-    if (f.colpairs)
+    if (f.colpairs) {
         GSR_TRY(grow(ctx, ctx->tile_diff,
                      (size_t)kTileDiffBlocks * gsr_tile_diff_cells(f.gx, f.rows_tiles) * 4, s));
+        GSR_TRY(grow(ctx, ctx->blend_order,
+                     (size_t)gsr_blend_order_groups((uint32_t)f.T_strip) * 4, s));
+    }
 
     GsrPreprocessArgs &pa = f.pa;
     pa = GsrPreprocessArgs{};
@@ -399,11 +407,17 @@ int launch_second_stream(gsr_context *ctx, const Frame &f) {
     if (f.tmode == 1) GSR_HIP(hipEventRecord(f.evc[0], as), "hipEventRecord");
     // the tile ranges before the colour, so the colour overlaps the column count and scatter
     // rather than the depth sort (C3 two frames in flight 3,470 -> 3,600 frames/s)
-    if (f.colpairs)
+    // (column pairs: the ranges, then the blend's heaviest-first order of the tile groups)
+    if (f.colpairs) {
         GSR_HIP(gsr_launch_tile_ranges_aux(f.pa.strip_rect, f.P, f.gx, f.rows_tiles,
                                            static_cast<uint32_t *>(ctx->tile_diff.p),
                                            static_cast<uint2 *>(ctx->ranges_local.p), as),
                 "tile ranges launch");
+        GSR_HIP(gsr_launch_blend_order(static_cast<const uint2 *>(ctx->ranges_local.p),
+                                       (uint32_t)f.T_strip,
+                                       static_cast<uint32_t *>(ctx->blend_order.p), as),
+                "blend order launch");
+    }
     // colour waves per SIMD (gsr_launch_color): 3 below 4M Gaussians, else 4 (sweeps on MI355X,
     // C3 and a C4 strip, DESIGN.md decision 7)
     const int color_waves = f.P < (4 << 20) ? 3 : 4;
@@ -566,6 +580,8 @@ int launch_blend(gsr_context *ctx, const Frame &f, const gsr_raster_settings *st
     ba.cull = ctx->cull;
     ba.fast = ctx->fast;
     ba.id_mask = f.id_mask;
+    ba.order = f.colpairs && ctx->blend_order_on ? static_cast<const uint32_t *>(ctx->blend_order.p)
+                                                 : nullptr;  // (per-pair form: row-major)
     GSR_HIP(gsr_launch_blend(ba, f.s), "blend launch");
     return GSR_OK;
 }
@@ -723,7 +739,7 @@ void gsr_destroy(gsr_context *ctx) {
                       &ctx->rect_sorted, &ctx->pair_count,    &ctx->perm,       &ctx->ds_ctl,
                       &ctx->tile_keys,   &ctx->tile_vals,     &ctx->tile_keys_alt,
                       &ctx->tile_vals_alt, &ctx->ranges_local, &ctx->tile_diff, &ctx->col_hist,
-                      &ctx->color_ids};
+                      &ctx->color_ids, &ctx->blend_order};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &set : ctx->ev)

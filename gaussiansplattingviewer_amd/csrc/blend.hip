@@ -68,13 +68,64 @@ __device__ __forceinline__ bool may_touch(float x, float y, float A, float B, fl
 }
 
 // Block -> work item, XCD-aware: the hardware deals block b to XCD b % 8 (speed only, never
-// correctness); groups of kXcdGroup consecutive work items (four tiles' quadrants) go
-// round-robin over the XCDs, so each group shares one L2 while the image's heavy and light
-// regions are spread evenly over the 8 XCDs.
+// correctness); groups of kXcdGroup consecutive work items (four row-adjacent tiles' quadrants)
+// go round-robin over the XCDs, so each group shares one L2 while the image's heavy and light
+// regions are spread evenly over the 8 XCDs.  With `order` (k_blend_order) the groups are
+// dealt heaviest first: every wave of the last round is then a short one, and the kernel's
+// tail -- the last waves finishing on an emptying chip -- shrinks.
 constexpr uint32_t kXcdGroup = 16;
-__device__ __forceinline__ uint32_t xcd_work(uint32_t b) {
+__device__ __forceinline__ uint32_t xcd_work(uint32_t b, const uint32_t *order,
+                                             uint32_t n_groups) {
     const uint32_t x = b & 7u, l = b >> 3;
-    return ((l / kXcdGroup) * 8u + x) * kXcdGroup + l % kXcdGroup;
+    uint32_t g = (l / kXcdGroup) * 8u + x;
+    if (order && g < n_groups) g = order[g];
+    return g * kXcdGroup + l % kXcdGroup;
+}
+
+// Counting sort of the tile groups by a log-scale pair count, descending (one block; order
+// within a bucket is arbitrary and does not matter: each wave's output depends only on its own
+// quadrant).  Key: 32 steps per octave of (pairs + 1), 1024 buckets.
+constexpr int kOrderBuckets = 1024;
+__device__ __forceinline__ uint32_t order_key(const uint2 *ranges, uint32_t g, uint32_t n_tiles) {
+    uint32_t n = 0;
+    const uint32_t t0 = g * (kXcdGroup / 4u);
+#pragma unroll
+    for (uint32_t i = 0; i < kXcdGroup / 4u; ++i)
+        if (t0 + i < n_tiles) {
+            const uint2 r = ranges[t0 + i];
+            n += r.y - r.x;
+        }
+    const int k = (int)(__builtin_amdgcn_logf((float)n + 1.0f) * 32.0f);
+    return (uint32_t)(kOrderBuckets - 1 - min(k, kOrderBuckets - 1));
+}
+
+__global__ __launch_bounds__(1024) void k_blend_order(const uint2 *__restrict__ ranges,
+                                                      uint32_t n_tiles, uint32_t n_groups,
+                                                      uint32_t *__restrict__ order) {
+    __shared__ uint32_t s_h[kOrderBuckets];
+    __shared__ uint32_t s_w[16];
+    const int tid = threadIdx.x;
+    s_h[tid] = 0u;
+    __syncthreads();
+    for (uint32_t g = tid; g < n_groups; g += 1024) atomicAdd(&s_h[order_key(ranges, g, n_tiles)], 1u);
+    __syncthreads();
+    // exclusive scan of the 1024 bucket counts
+    const uint32_t c = s_h[tid];
+    uint32_t x = c;
+    const int lane = tid & 63, w = tid >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int i = 0; i < w; ++i) base += s_w[i];
+    s_h[tid] = base + x - c;
+    __syncthreads();
+    for (uint32_t g = tid; g < n_groups; g += 1024)
+        order[atomicAdd(&s_h[order_key(ranges, g, n_tiles)], 1u)] = g;
 }
 
 // One staged splat as the inner loop reads it: three 16-B LDS reads from one address (fast
@@ -106,7 +157,7 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
     constexpr bool kPair = kFast && !kContrib;  // paired colour / bound words (see staging)
 
     const uint32_t b = blockIdx.x;
-    const uint32_t work = xcd_work(b);
+    const uint32_t work = xcd_work(b, a.order, (n_work + kXcdGroup - 1) / kXcdGroup);
     if (work >= n_work) return;
     const int lane = threadIdx.x;
     const uint32_t tile = work >> 2, quad = work & 3u;
@@ -299,6 +350,18 @@ inline uint32_t xcd_grid(uint32_t n_work) {
 }
 
 }  // namespace
+
+uint32_t gsr_blend_order_groups(uint32_t n_tiles) {
+    return (4u * n_tiles + kXcdGroup - 1) / kXcdGroup;
+}
+
+hipError_t gsr_launch_blend_order(const uint2 *ranges, uint32_t n_tiles, uint32_t *order,
+                                  hipStream_t s) {
+    if (n_tiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_blend_order, dim3(1), dim3(1024), 0, s, ranges, n_tiles,
+                       gsr_blend_order_groups(n_tiles), order);
+    return hipGetLastError();
+}
 
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s) {
     if (a.rows_tiles == 0 || a.grid_x == 0) return hipSuccess;

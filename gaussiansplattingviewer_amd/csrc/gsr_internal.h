@@ -377,5 +377,11 @@ struct GsrBlendArgs {
     int cull;            // 0: no quadrant cull (identical output, tested)
     int fast;            // 1: folded-constant FMA arithmetic + raw v_exp_f32; 0: upstream order
     uint32_t id_mask;    // point_list word -> Gaussian id (packed pair lists; else ~0u)
+    const uint32_t *order;  // tile groups heaviest first (gsr_launch_blend_order), or nullptr
 };
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s);
+// The blend's dispatch order: the groups of 4 row-adjacent tiles (16 quadrant waves, one XCD)
+// by descending pair count, so the last waves to start are the short ones.
+uint32_t gsr_blend_order_groups(uint32_t n_tiles);
+hipError_t gsr_launch_blend_order(const uint2 *ranges, uint32_t n_tiles, uint32_t *order,
+                                  hipStream_t s);
