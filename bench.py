@@ -75,6 +75,9 @@ def parse():
     ap.add_argument("--inflight", type=int, default=2,
                     help="frames in flight (FramePipeline: own stream + context slot each); "
                          "1 = serial forwards")
+    ap.add_argument("--compact-sort", default="auto", choices=["auto", "0", "1"],
+                    help="GSR_OPT_COMPACT_SORT: compact the kept depth keys before sorting "
+                         "(auto: strips of >= 4M Gaussians)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU-oracle time to sample for cpu_baseline (whole frames; at least one)")
     return ap.parse_args()
@@ -103,12 +106,13 @@ class Scene:
             if i == 0:  # the GL view (math layout) the OpenGL backend's sort receives
                 self.gl_view0 = np.asarray(cam.get_view_matrix(), dtype=np.float32)
 
-    def render(self, step, tile_rows=None, slot=0, out_color=None):
+    def render(self, step, tile_rows=None, slot=0, out_color=None, radii=True):
         view, proj, campos, tx, ty, _ = self.cams[step % len(self.cams)]
         return rasterize_gaussians_native(self.bg, self.xyz, None, self.opacity, self.scale,
                                           self.rot, 1.0, None, view, proj, tx, ty, self.H, self.W,
                                           self.sh, self.deg, campos, False, False,
-                                          tile_rows=tile_rows, slot=slot, out_color=out_color)
+                                          tile_rows=tile_rows, slot=slot, out_color=out_color,
+                                          radii=radii)
 
 
 # Committed rocprofv3 profiles (tools/profile_config.sh on the GPU box, summarised here by
@@ -353,7 +357,9 @@ def main():
                 mine = layout[rank]
                 buf = gather.next_buffer(strip_pixel_rows(mine, H)[1])
                 if mine[1] > mine[0]:
-                    res = scene.render(i, mine, slot, out_color=buf)
+                    # a strip rank returns its image only: no radii, so Gaussians that miss the
+                    # strip skip the per-Gaussian work (gsr.h gsr_outputs.radii)
+                    res = scene.render(i, mine, slot, out_color=buf, radii=False)
                     K = res.num_rendered
                     row_pairs = tile_row_pairs(mine[1] - mine[0], local, slot)
                 else:  # more GPUs than tile rows: nothing to render
@@ -361,7 +367,7 @@ def main():
                 gather.submit(buf, layout)
                 balancer.observe(i, row_pairs)
                 return K
-            return scene.render(i, rows, slot).num_rendered
+            return scene.render(i, rows, slot, radii=rows is None).num_rendered
 
     def drain():
         while gather is not None and gather.pending:
@@ -373,6 +379,7 @@ def main():
     for c in ctxs:
         opt = lambda o, v: _lib.check(lib.gsr_set_option(c, o, v), "gsr_set_option")  # noqa: E731
         opt(_lib.GSR_OPT_BLEND_FAST, {"exact": 0, "fast": 1}[args.blend])
+        opt(_lib.GSR_OPT_COMPACT_SORT, {"auto": -1, "0": 0, "1": 1}[args.compact_sort])
 
     # Warmup (also sizes the workspace so the timed loop never allocates).
     for i in range(args.warmup):
@@ -418,7 +425,7 @@ def main():
     n_serial = min(args.steps, 100)
     t1 = time.perf_counter()
     for i in range(n_serial):
-        scene.render(i, rows)
+        scene.render(i, rows, radii=rows is None)
     torch.cuda.synchronize()
     serial_ms = 1e3 * (time.perf_counter() - t1) / n_serial
 
@@ -427,7 +434,7 @@ def main():
     _lib.check(lib.gsr_set_timing(ctx, 1), "gsr_set_timing")
     torch.cuda.synchronize()
     for i in range(min(args.steps, 30)):
-        scene.render(i, rows)
+        scene.render(i, rows, radii=rows is None)
     torch.cuda.synchronize()
     _lib.check(lib.gsr_stage_times(ctx, buf, len(names)), "gsr_stage_times")
     _lib.check(lib.gsr_set_timing(ctx, 0), "gsr_set_timing")

@@ -66,7 +66,10 @@ constexpr auto kSpinLimit = std::chrono::milliseconds(50);
 // Frames with at least this many pairs wait for D before queueing the depth sort's later passes
 // (an empty third pass stays off the GPU: C3 3,480 vs 3,340 frames/s); smaller frames are bound
 // by the host's submission rate, which the wait would hold to the GPU (DESIGN.md §3 decision 2).
-constexpr int64_t kWaitDPairs = 4 << 20;
+#ifndef GSR_LAB_WAIT_D_PAIRS
+#define GSR_LAB_WAIT_D_PAIRS (4 << 20)
+#endif
+constexpr int64_t kWaitDPairs = GSR_LAB_WAIT_D_PAIRS;
 // The depth sort compacts the kept keys first on strips of at least this many Gaussians
 // (GSR_OPT_COMPACT_SORT auto): a 1/8 strip of C4 keeps ~1/8 of them (DESIGN.md decision 2).
 constexpr int64_t kCompactP = 4 << 20;
@@ -251,8 +254,12 @@ int setup_frame(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     const int W = st->image_width, H = st->image_height;
     if (P < 0 || P > (int64_t)UINT32_MAX) return fail(GSR_E_INVALID, "gsr_forward: bad P");
     if (W <= 0 || H <= 0) return fail(GSR_E_INVALID, "gsr_forward: image size must be positive");
-    if (!out->color || (P > 0 && !out->radii))
-        return fail(GSR_E_INVALID, "gsr_forward: color and radii outputs are required");
+    const bool strip = st->tile_row_begin != 0 || st->tile_row_end != 0;
+    const bool per_gaussian = out->depths || out->means2D || out->conic_opacity || out->rgb ||
+                              out->tiles_touched;
+    if (!out->color || (P > 0 && !out->radii && (!strip || per_gaussian)))
+        return fail(GSR_E_INVALID, "gsr_forward: color and radii outputs are required (radii "
+                                   "may be NULL only on a strip without per-Gaussian outputs)");
     if (P > 0) {
         if (!g->means3D || !g->opacities)
             return fail(GSR_E_INVALID, "gsr_forward: means3D and opacities are required");
@@ -348,6 +355,7 @@ int setup_frame(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     pa.sh_vec4 = (g->shs && g->M == 16 && (reinterpret_cast<uintptr_t>(g->shs) & 15) == 0) ? 1 : 0;
     pa.rot_vec4 = (g->rotations && (reinterpret_cast<uintptr_t>(g->rotations) & 15) == 0) ? 1 : 0;
     pa.radii = out->radii;
+    pa.strip_skip = out->radii == nullptr ? 1 : 0;
     pa.records = static_cast<gsr::SplatRecord *>(ctx->records.p);
     pa.sort_keys = static_cast<uint32_t *>(ctx->sort_keys.p);
     f.compact_sort = ctx->compact_sort < 0 ? (f.rows_tiles < f.gy && P >= kCompactP)
@@ -420,7 +428,11 @@ int launch_second_stream(gsr_context *ctx, const Frame &f) {
     }
     // colour waves per SIMD (gsr_launch_color): 3 below 4M Gaussians, else 4 (sweeps on MI355X,
     // C3 and a C4 strip, DESIGN.md decision 7)
+#ifdef GSR_LAB_COLOR_WAVES
+    const int color_waves = GSR_LAB_COLOR_WAVES;
+#else
     const int color_waves = f.P < (4 << 20) ? 3 : 4;
+#endif
     if (f.color_ids) {
         GSR_HIP(hipStreamWaitEvent(as, ctx->compacted, 0), "hipStreamWaitEvent(compacted)");
         GSR_HIP(gsr_launch_color_ids(f.pa, static_cast<const uint32_t *>(ctx->color_ids.p),

@@ -207,7 +207,8 @@ struct GsrPreprocessArgs {
     int prefiltered;
     int sh_vec4, rot_vec4;  // 16-B aligned rows: vector loads allowed
     // workspace outputs
-    int32_t *radii;
+    int32_t *radii;  // nullptr on a strip without radii: strip_skip
+    int strip_skip;  // skip Gaussians whose footprint bound misses the strip (preprocess.hip)
     gsr::SplatRecord *records;
     uint32_t *sort_keys;  // depth keys (0xFFFFFFFF: no pair in the strip); values are indices
     uint32_t *block_kept; // optional: per 256-Gaussian block, its count of kept keys

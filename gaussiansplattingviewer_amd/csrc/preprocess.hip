@@ -192,6 +192,35 @@ __device__ __forceinline__ float3 cull_data(float A, float B, float C, float o) 
     return make_float3(ex, ey, __uint_as_float(__float_as_uint(Lm) + 1u));
 }
 
+// Strip ranks without radii (strip_skip): may the Gaussian at view-space t with 3D covariance
+// c[6] and pixel row py have a tile in the strip?  False only when provably not: from an upper
+// bound of upstream's radius ceil(3 sqrt(lambda_max)) -- lambda_max of the 2D covariance
+// J W Sigma W^T J^T + 0.3 I is at most ||Sigma||_F ||W||_F^2 ||J||_F^2 + 0.3 sqrt(2), upstream's
+// eigenvalue formula adds at most sqrt(0.1), ||J||_F^2 <= (fx^2 (1 + limx^2) + fy^2 (1 +
+// limy^2)) / z^2 (the clamped J), with 1 % and 2 px of slack for float rounding -- through
+// get_rect, which is monotone in the radius.  NaN / inf anywhere keeps the Gaussian.
+__device__ __forceinline__ bool strip_reach(const GsrPreprocessArgs &a, float3 t, const float c[6],
+                                            float py) {
+    const float *vm = a.viewmatrix;
+    float wf = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 11; ++i)
+        if ((i & 3) != 3) wf = __builtin_fmaf(vm[i], vm[i], wf);
+    const float limx = 1.3f * a.tanfovx, limy = 1.3f * a.tanfovy;
+    const float jf = (a.focal_x * a.focal_x * (1.0f + limx * limx) +
+                      a.focal_y * a.focal_y * (1.0f + limy * limy)) *
+                     __builtin_amdgcn_rcpf(t.z * t.z);
+    const float sf2 = c[0] * c[0] + c[3] * c[3] + c[5] * c[5] +
+                      2.0f * (c[1] * c[1] + c[2] * c[2] + c[4] * c[4]);
+    const float lam = (__builtin_sqrtf(sf2) * wf * jf + 0.43f) * 1.01f + 0.32f;
+    if (!(lam < 1e30f)) return true;
+    const int r = f2i_sat(__builtin_ceilf(3.0f * __builtin_sqrtf(lam) * 1.01f + 2.0f));
+    const uint32_t y0 = min(a.grid_y, (uint32_t)max(0, f2i_sat((py - r) / GSR_TILE_Y)));
+    const uint32_t y1 =
+        min(a.grid_y, (uint32_t)max(0, f2i_sat((py + r + GSR_TILE_Y - 1) / GSR_TILE_Y)));
+    return y1 > y0 && y1 > a.row_begin && y0 < a.row_end;
+}
+
 // Returns the number of (Gaussian, strip tile) pairs of Gaussian idx.
 __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, int64_t idx,
                                                    uint32_t &key_out) {
@@ -227,6 +256,8 @@ __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, i
         } else {
             compute_cov3d(s_in, a.scale_modifier, q_in, cov3d);
         }
+        if (a.strip_skip && !strip_reach(a, p_view, cov3d, ndc2pix(p_proj_y, a.H)))
+            goto done;  // no tile in the strip: key, rect and pair count stay "none"
         const float3 cov = compute_cov2d(p_view, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy,
                                          cov3d, a.viewmatrix);
         const float det = cov.x * cov.z - cov.y * cov.y;
@@ -272,7 +303,8 @@ __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, i
             }
         }
     }
-    a.radii[idx] = radius_out;
+done:
+    if (a.radii) a.radii[idx] = radius_out;
     a.strip_rect[idx] = strip_rect;
     a.sort_keys[idx] = key;  // the depth sort's values are the indices (implicit)
     key_out = key;

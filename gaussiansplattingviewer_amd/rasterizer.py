@@ -69,7 +69,7 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
                                scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tanfovx,
                                tanfovy, image_height, image_width, sh, degree, campos, prefiltered,
                                debug, *, tile_rows=None, extras=(), stream=None, slot=0,
-                               out_color=None) -> ForwardResult:
+                               out_color=None, radii=True) -> ForwardResult:
     """Same arguments, order and validation as upstream `_C.rasterize_gaussians`.
 
     Extensions (keyword-only, for the strip partition and the parity tests):
@@ -78,10 +78,16 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
                    tiles_touched, final_T, n_contrib;
       stream    -- HIP stream handle (default: torch's current stream);
       slot      -- context slot (`_lib.context`): forwards in different slots may overlap;
-      out_color -- preallocated contiguous f32 (3, rows, W) output (e.g. a gather buffer).
+      out_color -- preallocated contiguous f32 (3, rows, W) output (e.g. a gather buffer);
+      radii     -- False (strips only, no per-Gaussian extras): no radii output
+                   (ForwardResult.radii is None); Gaussians whose footprint bound misses the
+                   strip skip the per-Gaussian work (a multi-GPU strip rank needs its image only).
     """
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    if not radii and (tile_rows is None or any(
+            n in extras for n in ("depths", "means2D", "conic_opacity", "rgb", "tiles_touched"))):
+        raise RuntimeError("radii=False needs tile_rows and no per-Gaussian extras")
     device = _device_of(means3D)
     dev_index = device.index if device.index is not None else torch.cuda.current_device()
     P = int(means3D.size(0))
@@ -122,7 +128,7 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
             raise RuntimeError(f"out_color must be a contiguous float32 (3, {rows}, {W}) tensor "
                                f"on {device}")
         color = out_color
-    radii = torch.empty((P,), dtype=torch.int32, device=device)
+    radii = torch.empty((P,), dtype=torch.int32, device=device) if radii else None
     ext = {}
     for name in extras:
         if name == "depths":
@@ -152,7 +158,8 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
                                 projmatrix=_lib.ptr(projmatrix), campos=_lib.ptr(campos),
                                 bg=_lib.ptr(bg), tile_row_begin=rb, tile_row_end=re,
                                 prefiltered=int(bool(prefiltered)), debug=int(bool(debug)))
-    out = _lib.GsrOutputs(color=color.data_ptr(), radii=radii.data_ptr() if P else None)
+    out = _lib.GsrOutputs(color=color.data_ptr(),
+                          radii=radii.data_ptr() if P and radii is not None else None)
     for name, t in ext.items():
         setattr(out, name, t.data_ptr())
     if stream is None:

@@ -86,7 +86,11 @@ typedef struct {
 
 typedef struct {
     float *color;    /* required: [3, rows, W] float32 (CHW, as upstream out_color) */
-    int32_t *radii;  /* required: [P] int32 (0 = culled) */
+    /* [P] int32 (0 = culled).  Required for whole frames.  On a strip (tile_row_begin/end)
+     * it may be NULL when no per-Gaussian intermediate below is requested either: Gaussians
+     * whose conservative footprint bound misses the strip then skip the covariance, radius and
+     * record work (a multi-GPU strip rank needs only its image). */
+    int32_t *radii;
     /* optional per-Gaussian intermediates (NULL = not written) */
     float *depths;        /* [P]   view-space z */
     float *means2D;       /* [P,2] pixel-space centre */

@@ -32,7 +32,7 @@ def to_dev(a, dev):
 
 
 def run_hip(s, dev, tile_rows=None, colors_precomp=None, cov3D_precomp=None, extras=ALL_EXTRAS,
-            binning=True, debug=False):
+            binning=True, debug=False, radii=True):
     g = s["g"]
     P = len(g.xyz)
     sh = None if colors_precomp is not None else to_dev(g.sh.reshape(P, g.sh.shape[-1] // 3, 3), dev)
@@ -43,9 +43,9 @@ def run_hip(s, dev, tile_rows=None, colors_precomp=None, cov3D_precomp=None, ext
         to_dev(g.rot, dev) if use_sr else None, s["scale_modifier"], to_dev(cov3D_precomp, dev),
         to_dev(s["view"], dev), to_dev(s["proj"], dev), s["tx"], s["ty"], s["H"], s["W"], sh,
         s["sh_degree"], to_dev(s["campos"], dev), False, debug, tile_rows=tile_rows,
-        extras=extras)
+        extras=extras, radii=radii)
     out = {"num_rendered": res.num_rendered, "color": res.color.cpu().numpy(),
-           "radii": res.radii.cpu().numpy()}
+           "radii": None if res.radii is None else res.radii.cpu().numpy()}
     for k, v in res.extras.items():
         out[k] = v.cpu().numpy()
     if "tiles_touched" in out:

@@ -96,6 +96,14 @@ def test_rasterizer_argument_checks_match_upstream():
           scales=torch.ones(4, 3), rotations=torch.ones(4, 4), cov3D_precomp=torch.ones(4, 6))
 
 
+def test_native_radii_optional_only_on_strips():
+    with pytest.raises(RuntimeError, match="radii=False needs tile_rows"):
+        rasterize_gaussians_native(torch.zeros(3), torch.zeros(4, 3), None, torch.ones(4, 1),
+                                   torch.ones(4, 3), torch.ones(4, 4), 1.0, None, torch.eye(4),
+                                   torch.eye(4), 0.5, 0.5, 8, 8, None, 0, torch.zeros(3), False,
+                                   False, radii=False)
+
+
 def test_native_rejects_bad_means_shape():
     with pytest.raises(RuntimeError, match=r"means3D must have dimensions \(num_points, 3\)"):
         rasterize_gaussians_native(torch.zeros(3), torch.zeros(4, 4), None, torch.ones(4, 1),

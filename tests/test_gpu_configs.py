@@ -124,6 +124,29 @@ def test_c4_strips_equal_full_frame_rows(gpu, c4, c4_hip, rank):
                                   full["ranges"][t0:t1][nonempty] - lo)
 
 
+@pytest.mark.parametrize("rank", [0, 3, 7])
+def test_c4_strips_without_radii(gpu, c4, c4_hip, rank):
+    """A strip rank without the radii output (gsr_outputs.radii NULL, the multi-GPU bench's
+    call) skips the Gaussians whose footprint bound misses its strip -- here with the C4 strips'
+    compaction and colour-id path: image and binning stay bit-identical to the full frame."""
+    s, _ = c4
+    full = c4_hip
+    W, H = s["W"], s["H"]
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    rows = strip_rows(gy, 8, rank)
+    part = run_hip(s, gpu, tile_rows=rows, extras=("final_T", "n_contrib"), radii=False)
+    assert part["radii"] is None
+    y0, n = strip_pixel_rows(rows, H)
+    np.testing.assert_array_equal(part["color"].view(np.uint32),
+                                  full["color"][:, y0:y0 + n].view(np.uint32))
+    np.testing.assert_array_equal(part["n_contrib"], full["n_contrib"][y0:y0 + n])
+    t0, t1 = rows[0] * gx, rows[1] * gx
+    lo = int(np.searchsorted(full["point_tiles"], t0))
+    hi = int(np.searchsorted(full["point_tiles"], t1))
+    assert part["num_rendered"] == hi - lo
+    np.testing.assert_array_equal(part["point_list"], full["point_list"][lo:hi])
+
+
 # ---- C3 with a capture-like scene (gaussian_data.clustered_scene) ----------------------------
 # BASELINE configs[2] quotes "bicycle PLY scale"; no PLY exists offline, so this scene stands in
 # for one: clustered centres, a ground plane under and behind the camera, a far background
@@ -175,3 +198,10 @@ def test_c3r_balanced_strips_bit_identical(gpu, c3r, c3r_hip):
         np.testing.assert_array_equal(part["color"].view(np.uint32),
                                       full["color"][:, y0:y0 + n].view(np.uint32))
         np.testing.assert_array_equal(part["n_contrib"], full["n_contrib"][y0:y0 + n])
+        # the bench's strip call: no radii, Gaussians that miss the strip skipped (near
+        # floaters, the ground plane and the background shell stress the footprint bound)
+        lean = run_hip(s, gpu, tile_rows=rows, extras=("final_T", "n_contrib"), radii=False)
+        np.testing.assert_array_equal(lean["color"].view(np.uint32),
+                                      part["color"].view(np.uint32))
+        np.testing.assert_array_equal(lean["n_contrib"], part["n_contrib"])
+        assert lean["num_rendered"] == part["num_rendered"]

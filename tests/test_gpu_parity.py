@@ -209,6 +209,10 @@ def test_strips_equal_full_frame_rows(gpu, world):
         np.testing.assert_array_equal(part["point_list"], full["point_list"][sel])
         np.testing.assert_array_equal(part["point_tiles"], full["point_tiles"][sel])
         K_sum += part["num_rendered"]
+        # without radii (a strip rank's call): Gaussians that miss the strip are skipped
+        lean = run_hip(s, gpu, tile_rows=rows, extras=("final_T", "n_contrib"), radii=False)
+        for k in ("color", "n_contrib", "final_T", "point_list", "ranges"):
+            np.testing.assert_array_equal(lean[k], part[k], err_msg=k)
     assert K_sum == full["num_rendered"]
 
 
@@ -389,5 +393,8 @@ def test_compacted_strip_colour_path(gpu):
                          ("n_contrib", full["n_contrib"][y0:y0 + n])):
                 np.testing.assert_array_equal(part[k].view(np.uint32), v.view(np.uint32), err_msg=k)
             np.testing.assert_array_equal(part["radii"], full["radii"])
+            lean = run_hip(s, gpu, tile_rows=rows, extras=pix, radii=False)
+            for k in ("color", "final_T", "n_contrib", "point_list"):
+                np.testing.assert_array_equal(lean[k], part[k], err_msg=k)
     finally:
         _set_option(gpu, _lib.GSR_OPT_COMPACT_SORT, -1)
