@@ -66,10 +66,7 @@ constexpr auto kSpinLimit = std::chrono::milliseconds(50);
 // Frames with at least this many pairs wait for D before queueing the depth sort's later passes
 // (an empty third pass stays off the GPU: C3 3,480 vs 3,340 frames/s); smaller frames are bound
 // by the host's submission rate, which the wait would hold to the GPU (DESIGN.md §3 decision 2).
-#ifndef GSR_LAB_WAIT_D_PAIRS
-#define GSR_LAB_WAIT_D_PAIRS (4 << 20)
-#endif
-constexpr int64_t kWaitDPairs = GSR_LAB_WAIT_D_PAIRS;
+constexpr int64_t kWaitDPairs = 4 << 20;
 // The depth sort compacts the kept keys first on strips of at least this many Gaussians
 // (GSR_OPT_COMPACT_SORT auto): a 1/8 strip of C4 keeps ~1/8 of them (DESIGN.md decision 2).
 constexpr int64_t kCompactP = 4 << 20;
@@ -112,10 +109,6 @@ struct gsr_context {
     int cull = 1;
     int fast = 1;
     int column_pairs = 1;
-#ifndef GSR_BLEND_ORDER_DEFAULT
-#define GSR_BLEND_ORDER_DEFAULT 1
-#endif
-    int blend_order_on = GSR_BLEND_ORDER_DEFAULT;  // (lab A/B builds set it to 0)
     int compact_sort = -1;
     // stage timing: a ring of event sets, one per timed forward, read back after the timed region
     int timing = 0;        // 0 off, 1 every stage, 2 the blend only, on every 8th forward
@@ -428,11 +421,7 @@ int launch_second_stream(gsr_context *ctx, const Frame &f) {
     }
     // colour waves per SIMD (gsr_launch_color): 3 below 4M Gaussians, else 4 (sweeps on MI355X,
     // C3 and a C4 strip, DESIGN.md decision 7)
-#ifdef GSR_LAB_COLOR_WAVES
-    const int color_waves = GSR_LAB_COLOR_WAVES;
-#else
     const int color_waves = f.P < (4 << 20) ? 3 : 4;
-#endif
     if (f.color_ids) {
         GSR_HIP(hipStreamWaitEvent(as, ctx->compacted, 0), "hipStreamWaitEvent(compacted)");
         GSR_HIP(gsr_launch_color_ids(f.pa, static_cast<const uint32_t *>(ctx->color_ids.p),
@@ -592,8 +581,8 @@ int launch_blend(gsr_context *ctx, const Frame &f, const gsr_raster_settings *st
     ba.cull = ctx->cull;
     ba.fast = ctx->fast;
     ba.id_mask = f.id_mask;
-    ba.order = f.colpairs && ctx->blend_order_on ? static_cast<const uint32_t *>(ctx->blend_order.p)
-                                                 : nullptr;  // (per-pair form: row-major)
+    ba.order = f.colpairs ? static_cast<const uint32_t *>(ctx->blend_order.p)
+                          : nullptr;  // (per-pair form: row-major)
     GSR_HIP(gsr_launch_blend(ba, f.s), "blend launch");
     return GSR_OK;
 }
