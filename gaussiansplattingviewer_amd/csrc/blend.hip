@@ -55,15 +55,19 @@ __device__ __forceinline__ bool may_touch(float x, float y, float A, float B, fl
     const float ulo = bx0 - x, uhi = bx1 - x, vlo = by0 - y, vhi = by1 - y;
     if (fmaxf(fmaxf(ulo, -uhi), 0.0f) > ex || fmaxf(fmaxf(vlo, -vhi), 0.0f) > ey) return false;
     if (ulo <= 0.0f && uhi >= 0.0f && vlo <= 0.0f && vhi >= 0.0f) return true;
-    // centre outside the box: q is convex, so its minimum over the box lies on an edge, where
-    // it is the 1-D minimum clamped to the edge.  The minimiser's slope -B/C (-B/A) comes from
+    // centre outside the box: q is convex, so its minimum over the box lies on an edge whose
+    // constraint the centre violates (at the minimiser, the direction to the centre leaves the
+    // box through an active face), where it is the 1-D minimum clamped to the edge: at most one
+    // vertical and one horizontal edge.  The minimiser's slope -B/C (-B/A) comes from
     // v_rcp_f32 (1 ulp) instead of an IEEE division (~10 VALU): a minimiser a few ulp off
     // raises q there by C * dv^2 ~ 1e-13 * q, far inside q_lower's 16-ulp rounding margin.
     const float su = -B * __builtin_amdgcn_rcpf(C), sv = -B * __builtin_amdgcn_rcpf(A);
-    float lb = q_lower(A, B, C, ulo, fminf(fmaxf(su * ulo, vlo), vhi));
-    lb = fminf(lb, q_lower(A, B, C, uhi, fminf(fmaxf(su * uhi, vlo), vhi)));
-    lb = fminf(lb, q_lower(A, B, C, fminf(fmaxf(sv * vlo, ulo), uhi), vlo));
-    lb = fminf(lb, q_lower(A, B, C, fminf(fmaxf(sv * vhi, ulo), uhi), vhi));
+    const float ue = ulo > 0.0f ? ulo : uhi, ve = vlo > 0.0f ? vlo : vhi;
+    const float lu = q_lower(A, B, C, ue, fminf(fmaxf(su * ue, vlo), vhi));
+    const float lv = q_lower(A, B, C, fminf(fmaxf(sv * ve, ulo), uhi), ve);
+    const float inf = __builtin_huge_valf();
+    const float lb = fminf((ulo > 0.0f || uhi < 0.0f) ? lu : inf,
+                           (vlo > 0.0f || vhi < 0.0f) ? lv : inf);
     return !(lb > twoL);
 }
 
