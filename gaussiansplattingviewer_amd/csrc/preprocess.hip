@@ -221,19 +221,21 @@ __device__ __forceinline__ bool strip_reach(const GsrPreprocessArgs &a, float3 t
     return y1 > y0 && y1 > a.row_begin && y0 < a.row_end;
 }
 
-// Returns the number of (Gaussian, strip tile) pairs of Gaussian idx.
-__device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, int64_t idx,
-                                                   uint32_t &key_out) {
-    int32_t radius_out = 0;
-    uint32_t strip_tiles = 0, all_tiles = 0;
-    uint2 strip_rect = make_uint2(0u, 0u);
-    uint32_t key = 0xFFFFFFFFu;
+// The first half of upstream preprocessCUDA for one Gaussian: every input loaded up front (so
+// all loads are in flight together instead of a second round trip after the frustum test),
+// the frustum test, the projection and the 3D covariance.
+struct Front {
+    float3 p_view;
+    float p_proj_x, p_proj_y;
+    float cov3d[6];
+    float opacity;
+    bool in_frustum;
+};
 
+__device__ __forceinline__ Front front_one(const GsrPreprocessArgs &a, int64_t idx) {
+    Front f;
     const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1],
                                  a.means3D[3 * idx + 2]);
-    // every per-Gaussian input is loaded up front, so all loads are in flight together instead
-    // of a second round trip after the frustum test (they are needed for every Gaussian in
-    // the frustum: all of them at C3)
     float3 s_in = make_float3(0.f, 0.f, 0.f);
     float4 q_in = make_float4(0.f, 0.f, 0.f, 0.f);
     if (!a.cov3D_precomp) {
@@ -242,24 +244,44 @@ __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, i
                           : make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1],
                                         a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
     }
-    const float opacity_in = a.opacities[idx];
-    const float3 p_view = transform_point_4x3(p, a.viewmatrix);
-    if (p_view.z > 0.2f) {  // in_frustum
+    f.opacity = a.opacities[idx];
+    f.p_view = transform_point_4x3(p, a.viewmatrix);
+    f.in_frustum = f.p_view.z > 0.2f;
+    f.p_proj_x = f.p_proj_y = 0.0f;
+    if (f.in_frustum) {
         const float4 p_hom = transform_point_4x4(p, a.projmatrix);
         const float p_w = 1.0f / (p_hom.w + 0.0000001f);
-        const float p_proj_x = p_hom.x * p_w, p_proj_y = p_hom.y * p_w;
-
-        float cov3d[6];
+        f.p_proj_x = p_hom.x * p_w;
+        f.p_proj_y = p_hom.y * p_w;
         if (a.cov3D_precomp) {
 #pragma unroll
-            for (int i = 0; i < 6; ++i) cov3d[i] = a.cov3D_precomp[6 * idx + i];
+            for (int i = 0; i < 6; ++i) f.cov3d[i] = a.cov3D_precomp[6 * idx + i];
         } else {
-            compute_cov3d(s_in, a.scale_modifier, q_in, cov3d);
+            compute_cov3d(s_in, a.scale_modifier, q_in, f.cov3d);
         }
-        if (a.strip_skip && !strip_reach(a, p_view, cov3d, ndc2pix(p_proj_y, a.H)))
-            goto done;  // no tile in the strip: key, rect and pair count stay "none"
+    }
+    return f;
+}
+
+// The outputs of a Gaussian without a pair in the strip (strip_skip: radii and the
+// per-Gaussian extras are not requested).
+__device__ __forceinline__ void none_one(const GsrPreprocessArgs &a, int64_t idx) {
+    a.strip_rect[idx] = make_uint2(0u, 0u);
+    a.sort_keys[idx] = 0xFFFFFFFFu;
+}
+
+// The second half: 2D covariance, conic, radius, tile rect, depth key, the blend's record.
+// Returns the number of (Gaussian, strip tile) pairs of Gaussian idx.
+__device__ __forceinline__ uint32_t back_one(const GsrPreprocessArgs &a, int64_t idx,
+                                             const Front &f, uint32_t &key_out) {
+    int32_t radius_out = 0;
+    uint32_t strip_tiles = 0, all_tiles = 0;
+    uint2 strip_rect = make_uint2(0u, 0u);
+    uint32_t key = 0xFFFFFFFFu;
+    if (f.in_frustum) {
+        const float3 p_view = f.p_view;
         const float3 cov = compute_cov2d(p_view, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy,
-                                         cov3d, a.viewmatrix);
+                                         f.cov3d, a.viewmatrix);
         const float det = cov.x * cov.z - cov.y * cov.y;
         if (det != 0.0f) {
             const float det_inv = 1.f / det;
@@ -269,12 +291,12 @@ __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, i
             const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
             const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
             const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
-            const float px = ndc2pix(p_proj_x, a.W), py = ndc2pix(p_proj_y, a.H);
+            const float px = ndc2pix(f.p_proj_x, a.W), py = ndc2pix(f.p_proj_y, a.H);
             const int r_int = f2i_sat(my_radius);
             const Rect rc = get_rect(px, py, r_int, a.grid_x, a.grid_y);
             all_tiles = (rc.x1 - rc.x0) * (rc.y1 - rc.y0);
             if (all_tiles != 0) {
-                const float opacity = opacity_in;
+                const float opacity = f.opacity;
                 radius_out = r_int;
                 const uint32_t sy0 = max(rc.y0, a.row_begin), sy1 = min(rc.y1, a.row_end);
                 strip_tiles = sy1 > sy0 ? (rc.x1 - rc.x0) * (sy1 - sy0) : 0u;
@@ -303,7 +325,6 @@ __device__ __forceinline__ uint32_t preprocess_one(const GsrPreprocessArgs &a, i
             }
         }
     }
-done:
     if (a.radii) a.radii[idx] = radius_out;
     a.strip_rect[idx] = strip_rect;
     a.sort_keys[idx] = key;  // the depth sort's values are the indices (implicit)
@@ -312,15 +333,74 @@ done:
     return strip_tiles;
 }
 
+// strip_skip: the block's Gaussians that may reach the strip, compacted (their Front in LDS,
+// structure of arrays) so the second half runs on as few waves as hold them -- on a 1/8 strip
+// about one wave in four -- instead of on every wave that has one such lane.
+struct SkipSmem {
+    float v[12][256];  // p_view xyz, p_proj xy, cov3d[6], opacity
+    uint32_t idx[256];
+    uint32_t wcount[4];
+};
+
 // One thread per Gaussian.  Block b also stores its share of K (the (Gaussian, strip tile)
 // pair count) and the OR / AND of its kept depth keys (k_publish_K reduces them for the host:
 // K sizes the binning, bits(OR ^ AND) the depth sort's passes), and with a.block_kept (the
 // depth sort's compaction, strips) how many of its 256 Gaussians have pairs in the strip.
 // (A separate pass re-reading the rects and keys took 7 us at C3 and 42 us on a C4 strip.)
+template <bool kSkip>
 __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t key = 0xFFFFFFFFu;
-    const uint32_t pairs = idx < a.P ? preprocess_one(a, idx, key) : 0u;
+    uint32_t pairs = 0u;
+    if (!kSkip) {
+        if (idx < a.P) pairs = back_one(a, idx, front_one(a, idx), key);
+    } else {
+        __shared__ SkipSmem sk;
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        bool reach = false;
+        Front f;
+        if (idx < a.P) {
+            f = front_one(a, idx);
+            reach = f.in_frustum &&
+                    strip_reach(a, f.p_view, f.cov3d, ndc2pix(f.p_proj_y, a.H));
+            if (!reach) none_one(a, idx);
+        }
+        const uint64_t bal = __ballot(reach);
+        if (lane == 0) sk.wcount[w] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t base = 0, n = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            base += i < w ? sk.wcount[i] : 0u;
+            n += sk.wcount[i];
+        }
+        if (reach) {
+            const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+            const uint32_t slot = base + (uint32_t)__popcll(bal & lt);
+            sk.v[0][slot] = f.p_view.x;
+            sk.v[1][slot] = f.p_view.y;
+            sk.v[2][slot] = f.p_view.z;
+            sk.v[3][slot] = f.p_proj_x;
+            sk.v[4][slot] = f.p_proj_y;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) sk.v[5 + i][slot] = f.cov3d[i];
+            sk.v[11][slot] = f.opacity;
+            sk.idx[slot] = (uint32_t)idx;
+        }
+        __syncthreads();
+        if (threadIdx.x < n) {
+            const uint32_t t = threadIdx.x;
+            Front g;
+            g.p_view = make_float3(sk.v[0][t], sk.v[1][t], sk.v[2][t]);
+            g.p_proj_x = sk.v[3][t];
+            g.p_proj_y = sk.v[4][t];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) g.cov3d[i] = sk.v[5 + i][t];
+            g.opacity = sk.v[11][t];
+            g.in_frustum = true;
+            pairs = back_one(a, (int64_t)sk.idx[t], g, key);
+        }
+    }
     const bool kept = pairs != 0u;  // has pairs in the strip <=> its depth key is kept
     uint32_t v = pairs, o = kept ? key : 0u, an = kept ? key : 0xFFFFFFFFu;  // v <= 256 x 2^16
 #pragma unroll
@@ -342,6 +422,42 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
             make_uint2(s_red[1][0] | s_red[1][1] | s_red[1][2] | s_red[1][3],
                        s_red[2][0] & s_red[2][1] & s_red[2][2] & s_red[2][3]);
         if (a.block_kept) a.block_kept[blockIdx.x] = s_red[3][0] + s_red[3][1] + s_red[3][2] + s_red[3][3];
+    }
+}
+
+// Whole frames, two Gaussians per thread (128-thread blocks of 256 Gaussians, the same block
+// outputs): both Gaussians' loads are in flight together.
+__global__ __launch_bounds__(128) void k_preprocess2(const GsrPreprocessArgs a) {
+    const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x, i1 = i0 + 128;
+    uint32_t k0 = 0xFFFFFFFFu, k1 = 0xFFFFFFFFu;
+    Front f0, f1;
+    if (i0 < a.P) f0 = front_one(a, i0);
+    if (i1 < a.P) f1 = front_one(a, i1);
+    const uint32_t p0 = i0 < a.P ? back_one(a, i0, f0, k0) : 0u;
+    const uint32_t p1 = i1 < a.P ? back_one(a, i1, f1, k1) : 0u;
+    uint32_t v = p0 + p1;
+    uint32_t o = (p0 ? k0 : 0u) | (p1 ? k1 : 0u);
+    uint32_t an = (p0 ? k0 : 0xFFFFFFFFu) & (p1 ? k1 : 0xFFFFFFFFu);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        v += __shfl_xor(v, off);
+        o |= __shfl_xor(o, off);
+        an &= __shfl_xor(an, off);
+    }
+    __shared__ uint32_t s_red[4][2];
+    const uint32_t c = a.block_kept ? (uint32_t)(__popcll(__ballot(p0 != 0u)) +
+                                                 __popcll(__ballot(p1 != 0u)))
+                                    : 0u;
+    if ((threadIdx.x & 63) == 0) {
+        const int w = threadIdx.x >> 6;
+        s_red[0][w] = v, s_red[1][w] = o, s_red[2][w] = an, s_red[3][w] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a.block_pairs[blockIdx.x] = (uint64_t)s_red[0][0] + s_red[0][1];
+        reinterpret_cast<uint2 *>(a.block_pairs + gridDim.x)[blockIdx.x] =
+            make_uint2(s_red[1][0] | s_red[1][1], s_red[2][0] & s_red[2][1]);
+        if (a.block_kept) a.block_kept[blockIdx.x] = s_red[3][0] + s_red[3][1];
     }
 }
 
@@ -533,7 +649,15 @@ inline unsigned grid_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, hipStream_t s) {
     if (a.P == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_preprocess, dim3(grid_for(a.P)), dim3(256), 0, s, a);
+    if (a.strip_skip)
+        hipLaunchKernelGGL(k_preprocess<true>, dim3(grid_for(a.P)), dim3(256), 0, s, a);
+#ifdef GSR_LAB_PRE2
+    else
+        hipLaunchKernelGGL(k_preprocess2, dim3(grid_for(a.P)), dim3(128), 0, s, a);
+#else
+    else
+        hipLaunchKernelGGL(k_preprocess<false>, dim3(grid_for(a.P)), dim3(256), 0, s, a);
+#endif
     return hipGetLastError();
 }
 
