@@ -425,42 +425,6 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
     }
 }
 
-// Whole frames, two Gaussians per thread (128-thread blocks of 256 Gaussians, the same block
-// outputs): both Gaussians' loads are in flight together.
-__global__ __launch_bounds__(128) void k_preprocess2(const GsrPreprocessArgs a) {
-    const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x, i1 = i0 + 128;
-    uint32_t k0 = 0xFFFFFFFFu, k1 = 0xFFFFFFFFu;
-    Front f0, f1;
-    if (i0 < a.P) f0 = front_one(a, i0);
-    if (i1 < a.P) f1 = front_one(a, i1);
-    const uint32_t p0 = i0 < a.P ? back_one(a, i0, f0, k0) : 0u;
-    const uint32_t p1 = i1 < a.P ? back_one(a, i1, f1, k1) : 0u;
-    uint32_t v = p0 + p1;
-    uint32_t o = (p0 ? k0 : 0u) | (p1 ? k1 : 0u);
-    uint32_t an = (p0 ? k0 : 0xFFFFFFFFu) & (p1 ? k1 : 0xFFFFFFFFu);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        v += __shfl_xor(v, off);
-        o |= __shfl_xor(o, off);
-        an &= __shfl_xor(an, off);
-    }
-    __shared__ uint32_t s_red[4][2];
-    const uint32_t c = a.block_kept ? (uint32_t)(__popcll(__ballot(p0 != 0u)) +
-                                                 __popcll(__ballot(p1 != 0u)))
-                                    : 0u;
-    if ((threadIdx.x & 63) == 0) {
-        const int w = threadIdx.x >> 6;
-        s_red[0][w] = v, s_red[1][w] = o, s_red[2][w] = an, s_red[3][w] = c;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        a.block_pairs[blockIdx.x] = (uint64_t)s_red[0][0] + s_red[0][1];
-        reinterpret_cast<uint2 *>(a.block_pairs + gridDim.x)[blockIdx.x] =
-            make_uint2(s_red[1][0] | s_red[1][1], s_red[2][0] & s_red[2][1]);
-        if (a.block_kept) a.block_kept[blockIdx.x] = s_red[3][0] + s_red[3][1];
-    }
-}
-
 // One block, on the second stream after the preprocess (the kernel boundary makes its stores
 // visible): K = sum of the per-block pair counts and D = the bits in which the kept depth keys
 // differ (bits of OR ^ AND: the depth sort's pass count), stored straight into pinned host
@@ -651,13 +615,8 @@ hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, hipStream_t s) {
     if (a.P == 0) return hipSuccess;
     if (a.strip_skip)
         hipLaunchKernelGGL(k_preprocess<true>, dim3(grid_for(a.P)), dim3(256), 0, s, a);
-#ifdef GSR_LAB_PRE2
-    else
-        hipLaunchKernelGGL(k_preprocess2, dim3(grid_for(a.P)), dim3(128), 0, s, a);
-#else
     else
         hipLaunchKernelGGL(k_preprocess<false>, dim3(grid_for(a.P)), dim3(256), 0, s, a);
-#endif
     return hipGetLastError();
 }
 

@@ -197,6 +197,10 @@ class StripGather:
         self.pending.append(slot)
 
     def finish(self) -> torch.Tensor | None:
+        """Wait for the oldest submitted frame; on rank 0 return it (None elsewhere).  The
+        returned tensor is the slot's own frame buffer: it stays valid until that slot is
+        submitted again (`depth` submits later) -- clone it to keep it longer (e.g. in a display
+        queue)."""
         slot = self.pending.pop(0)
         for req in slot["reqs"]:
             req.wait()
