@@ -7,8 +7,10 @@
 // splat's conservative alpha >= 1/255 ellipse from preprocess.hip cull_data: bounding box,
 // then the exact ellipse-vs-box minimum with a rounding bound), compacts the survivors into
 // LDS with a ballot, composites them two at a time, and stops as soon as its 64 pixels are
-// done.  At C3 a quadrant composites ~11 % of its tile's list (SQ counters: ~2,900 VALU per
-// wave, ~95 % of them in the compositing loop, 21.5 VALU per pixel-splat).
+// done.  At C3 a quadrant wave examines ~4.4 chunks (~280 list entries) and composites ~118
+// splats (a per-wave timeline, tools/lab/blend_trace.py); by the ISA and SQ_INSTS_VALU about two
+// thirds of its VALU is the compositing loop (33 VALU + 5 LDS reads per composited pair) and one
+// third the per-chunk gather, cull and staging.
 //
 // Skipping splats that provably cannot reach alpha >= 1/255 changes nothing: upstream skips
 // them too (`if (alpha < 1/255) continue`), and n_contrib -- upstream's running `contributor`
