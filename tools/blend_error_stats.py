@@ -24,13 +24,14 @@ import torch  # noqa: E402
 import oracle  # noqa: E402
 from gaussiansplattingviewer_amd import _lib  # noqa: E402
 from gaussiansplattingviewer_amd.camera import orbit_eye, static_camera  # noqa: E402
-from gaussiansplattingviewer_amd.gaussian_data import synthetic_gaussians  # noqa: E402
+from gaussiansplattingviewer_amd.gaussian_data import clustered_scene, synthetic_gaussians  # noqa: E402
 from gpu_helpers import psnr_db, run_hip, run_oracle, scene_inputs  # noqa: E402
 
 # name: (P, W, H, sh_degree, seed, frames of the 1000-frame orbit or None for the static camera)
 CONFIGS = {"c1": (10_000, 640, 480, 3, 0, None), "c2": (100_000, 1920, 1080, 0, 1, None),
            "c3": (1_000_000, 1920, 1080, 3, 2, None), "c4": (6_000_000, 3840, 2160, 3, 3, None),
-           "c5": (1_000_000, 1920, 1080, 3, 2, (0, 250, 500, 750))}
+           "c5": (1_000_000, 1920, 1080, 3, 2, (0, 250, 500, 750)),
+           "c3r": (1_000_000, 1920, 1080, 3, 7, None)}  # gaussian_data.clustered_scene
 
 
 def stats(hip, orc):
@@ -52,7 +53,7 @@ def main():
     ctx = _lib.context(0)
     for name in a.configs.split(","):
         P, W, H, deg, seed, frames = CONFIGS[name]
-        g = synthetic_gaussians(P, deg, seed)
+        g = clustered_scene(P, seed) if name == "c3r" else synthetic_gaussians(P, deg, seed)
         for f in (frames or (None,)):
             eye = orbit_eye(f, 1000) if f is not None else (0.0, 0.0, 4.0)
             s = scene_inputs(g, static_camera(W, H, eye), deg)
