@@ -466,7 +466,11 @@ def main():
     # (two frames in flight, the other frame's kernels sharing the CUs) are reported beside it.
     dom_ms = stage_ms["blend"]
     default_opts = args.blend == "fast"  # the committed profiles are of the default arithmetic
-    roofline = blend_roofline(args.config if default_opts else None, dom_ms, blend_ms_timed,
+    # profiles are keyed by config (and the simulated strip: <tag>_<config>-strip<R><N>_*.json)
+    prof_key = args.config + (f"-strip{args.sim_strip.replace('/', '')}" if args.sim_strip else "")
+    if world > 1:
+        prof_key = None  # no profile of a rank's strip of a multi-GPU frame
+    roofline = blend_roofline(prof_key if default_opts else None, dom_ms, blend_ms_timed,
                               alg["blend"])
     roofline["frame_alg_gbs"] = round(sum(alg.values()) / (t_max / args.steps) / 1e9, 2)
     fps = args.steps / t_max

@@ -6,7 +6,7 @@
 # ends the script.  Writes gpurun_out/prof_${TAG}_${CONFIG}/ and the sha of the profiled
 # library (lib.sha); summarise here with
 #   python tools/prof_summary.py gpurun_out/prof_<tag>_<config> --json profiles/<tag>_<config>_kernels.json
-#   python tools/sq_summary.py gpurun_out/prof_<tag>_<config> k_blend --json profiles/<tag>_<config>_blend_sq.json
+#   python tools/sq_summary.py gpurun_out/prof_<tag>_<config> k_blend_q --json profiles/<tag>_<config>_blend_sq.json
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

@@ -23,7 +23,7 @@ names = set()
 for f in glob.glob(d + "/p[0-9]*/**/pmc_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         if kern in r["Kernel_Name"]:
-            names.add(r["Kernel_Name"].split("(")[0])
+            names.add(r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0])
             agg[r["Counter_Name"]][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
 res = {c: sum(v.values()) / len(v) for c, v in agg.items()}
 launches = {c: len(v) for c, v in agg.items()}
