@@ -18,6 +18,7 @@ import os
 import numpy as np
 import pytest
 
+from gaussiansplattingviewer_amd import _lib
 from gaussiansplattingviewer_amd.camera import Camera
 from gaussiansplattingviewer_amd.gaussian_data import synthetic_gaussians
 from gaussiansplattingviewer_amd.rasterizer import binning_state
@@ -66,10 +67,11 @@ def test_reference_viewer_pose(gpu, oracle_mod, viewer, i):
                              rotations=host(g.rot), bg=host(rs["bg"]))
     # every pose sees part of the scene except the last, saved 6.8 units out, looking away
     assert (orc["num_rendered"] > 0) == (i != 17)
-    assert len(pl) == orc["num_rendered"]
     np.testing.assert_array_equal(radii, orc["radii"])
-    np.testing.assert_array_equal(pl.cpu().numpy().view(np.uint32), orc["point_list"])
-    np.testing.assert_array_equal(pt.cpu().numpy().view(np.uint32),
-                                  (orc["point_keys"] >> np.uint64(32)).astype(np.uint32))
-    np.testing.assert_array_equal(rg.cpu().numpy().view(np.uint32), orc["ranges"])
+    if _lib._native_shares_library():  # not under a GSR_LIB A/B build: its own context
+        assert len(pl) == orc["num_rendered"]
+        np.testing.assert_array_equal(pl.cpu().numpy().view(np.uint32), orc["point_list"])
+        np.testing.assert_array_equal(pt.cpu().numpy().view(np.uint32),
+                                      (orc["point_keys"] >> np.uint64(32)).astype(np.uint32))
+        np.testing.assert_array_equal(rg.cpu().numpy().view(np.uint32), orc["ranges"])
     assert_image_close(img, orc["color"])
