@@ -19,6 +19,7 @@ GSR_OPT_BLEND_CULL = 1
 GSR_OPT_BLEND_FAST = 2
 GSR_OPT_COLUMN_PAIRS = 10
 GSR_OPT_COMPACT_SORT = 11
+GSR_OPT_TIGHT_BINNING = 12
 
 # Symbols include/gsr.h declares (checked by the CPU test suite).
 EXPORTED_SYMBOLS = (

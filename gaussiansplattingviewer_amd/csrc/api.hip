@@ -81,6 +81,7 @@ struct gsr_context {
     // per-Gaussian workspace
     DevBuf records, strip_rect, sort_keys, partials, total, hist, digit_total, bin, chunk_first,
         rect_sorted, pair_count;
+    DevBuf strip_rc, rc_sorted;  // tight binning: {rect, span word}, by id and in depth order
     DevBuf ds_a, ds_b;   // depth sort: (key, id) pairs between passes (ping-pong)
     DevBuf block_kept;   // depth sort compaction (strips): kept keys per 256-Gaussian block
     DevBuf color_ids;    // compacted strips: the kept ids the colour pass walks (4 B x P)
@@ -93,14 +94,17 @@ struct gsr_context {
     DevBuf tile_diff;  // difference-array partials of the second-stream tile ranges
     DevBuf blend_order;  // the blend's tile groups, heaviest first (second stream)
     // pinned host words the GPU stores into: [0] -, [1] -, [2] K (k_publish_K), [3] its depth-key
-    // bits, [4] (frame tag << 32) | D from the depth sort's pass 0, [5] -, [6] -, [7] K's tag
+    // bits, [4] (frame tag << 32) | D from the depth sort's pass 0, [5] the pair count over the
+    // spans (k_publish_K), [6] -, [7] K's tag
     uint64_t *h_total = nullptr;
     unsigned long long *d_hostK = nullptr;  // device view of h_total + 2
     unsigned long long *d_hostD = nullptr;  // device view of h_total + 4
     uint32_t sort_tag = 0;                  // frames rendered on this context (the pinned tags)
     // state of the last forward (gsr_get_binning, gsr_tile_row_pairs)
     bool have_forward = false;
-    int64_t last_K = 0;
+    int64_t last_K = 0;        // upstream's num_rendered
+    int64_t last_list = 0;     // pairs in the list (tight binning: fewer than last_K)
+    bool last_tight = false;
     uint32_t last_gx = 0, last_gy = 0, last_rb = 0, last_re = 0;
     uint32_t *last_point_list = nullptr, *last_tiles_local = nullptr;
     bool last_packed = false;             // column pairs: packed words, no tile-key array
@@ -110,6 +114,7 @@ struct gsr_context {
     int fast = 1;
     int column_pairs = 1;
     int compact_sort = -1;
+    int tight = 1;
     // stage timing: a ring of event sets, one per timed forward, read back after the timed region
     int timing = 0;        // 0 off, 1 every stage, 2 the blend only, on every 8th forward
     int64_t forwards = 0;  // forwards since gsr_set_timing (mode 2's sampling)
@@ -171,6 +176,8 @@ int reserve_P(gsr_context *ctx, int64_t P, hipStream_t s) {
     GSR_TRY(grow(ctx, ctx->ds_ctl, (size_t)gsr_depth_sort_ctl_words(P) * 4, s));
     GSR_TRY(grow(ctx, ctx->bin, n * 16, s));
     GSR_TRY(grow(ctx, ctx->rect_sorted, n * 8, s));
+    GSR_TRY(grow(ctx, ctx->strip_rc, n * 16, s));
+    GSR_TRY(grow(ctx, ctx->rc_sorted, n * 16, s));
     return GSR_OK;
 }
 
@@ -222,7 +229,9 @@ struct Frame {
     int col_shift;      // column pairs: packed word = strip row << col_shift | Gaussian id
     uint32_t tag;       // this frame's tag for the pinned words
     GsrPreprocessArgs pa;
-    uint64_t K = 0;
+    bool tight;  // tight binning: pairs only over the span words (needs the column-first form)
+    uint64_t K = 0;   // upstream's num_rendered
+    uint64_t KL = 0;  // pairs in the list (K, or fewer with tight binning)
     // the pair list the blend reads and gsr_get_binning exports
     uint32_t *point_list = nullptr, *tiles_local = nullptr;
     uint32_t id_mask = 0xFFFFFFFFu;
@@ -355,6 +364,10 @@ int setup_frame(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
                                            : ctx->compact_sort != 0;
     pa.block_kept = f.compact_sort ? static_cast<uint32_t *>(ctx->block_kept.p) : nullptr;
     pa.strip_rect = static_cast<uint2 *>(ctx->strip_rect.p);
+    // tight binning: the column-first form, and no n_contrib (upstream's n_contrib counts list
+    // positions of the full 3-sigma pairs); span words only then (NULL: every rect full)
+    f.tight = ctx->tight && f.colpairs && !out->n_contrib;
+    pa.strip_rc = f.tight ? static_cast<uint4 *>(ctx->strip_rc.p) : nullptr;
     pa.block_pairs = static_cast<uint64_t *>(ctx->pair_count.p);
     pa.host_K = ctx->d_hostK;
     pa.depths = out->depths;
@@ -410,7 +423,8 @@ int launch_second_stream(gsr_context *ctx, const Frame &f) {
     // rather than the depth sort (C3 two frames in flight 3,470 -> 3,600 frames/s)
     // (column pairs: the ranges, then the blend's heaviest-first order of the tile groups)
     if (f.colpairs) {
-        GSR_HIP(gsr_launch_tile_ranges_aux(f.pa.strip_rect, f.P, f.gx, f.rows_tiles,
+        GSR_HIP(gsr_launch_tile_ranges_aux(f.pa.strip_rect, f.pa.strip_rc, f.P, f.gx,
+                                           f.rows_tiles,
                                            static_cast<uint32_t *>(ctx->tile_diff.p),
                                            static_cast<uint2 *>(ctx->ranges_local.p), as),
                 "tile ranges launch");
@@ -444,7 +458,10 @@ int launch_scan(gsr_context *ctx, const Frame &f) {
     const uint32_t *d_valid = static_cast<const uint32_t *>(ctx->ds_ctl.p);
     uint2 *rect_sorted = static_cast<uint2 *>(ctx->rect_sorted.p);
     if (f.colpairs) {
-        GSR_HIP(gsr_launch_col_pairs_count(perm, f.pa.strip_rect, f.P, d_valid, rect_sorted,
+        GSR_HIP(gsr_launch_col_pairs_count(perm, f.pa.strip_rect, f.pa.strip_rc, f.P, d_valid,
+                                           rect_sorted,
+                                           f.tight ? static_cast<uint4 *>(ctx->rc_sorted.p)
+                                                   : nullptr,
                                            static_cast<uint32_t *>(ctx->col_hist.p),
                                            static_cast<uint32_t *>(ctx->digit_total.p), f.s),
                 "column count launch");
@@ -468,6 +485,7 @@ int wait_K(gsr_context *ctx, Frame &f) {
     if (!spin_on(&ctx->h_total[7], [&](uint64_t v) { return v == f.tag; }, tagv))
         GSR_HIP(hipStreamSynchronize(ctx->aux), "hipStreamSynchronize(pair count)");
     f.K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
+    f.KL = f.tight ? __atomic_load_n(&ctx->h_total[5], __ATOMIC_ACQUIRE) : f.K;
     if (f.dbg) {
         uint32_t ctl2[2];
         uint64_t scan_K[2] = {0, 0};
@@ -488,7 +506,7 @@ int wait_K(gsr_context *ctx, Frame &f) {
     }
     if (f.K > (uint64_t)UINT32_MAX - 4096)
         return fail(GSR_E_INVALID, "gsr_forward: more than 2^32-4097 (Gaussian, tile) pairs");
-    return reserve_K(ctx, (int64_t)f.K, f.s);
+    return reserve_K(ctx, (int64_t)f.KL, f.s);
 }
 
 // ---- 4 + 5. the pairs, stably sorted by strip tile ------------------------------------------
@@ -502,12 +520,15 @@ int launch_binning(gsr_context *ctx, Frame &f) {
     uint32_t *tv = static_cast<uint32_t *>(ctx->tile_vals.p);
     uint32_t *tk_alt = static_cast<uint32_t *>(ctx->tile_keys_alt.p);
     uint32_t *tv_alt = static_cast<uint32_t *>(ctx->tile_vals_alt.p);
-    const int64_t K = (int64_t)f.K;
+    const int64_t K = (int64_t)f.KL;
     if (f.colpairs) {
         // pass 1 by column on (Gaussian, column) segments, then pass 2 on the packed words'
         // row bits, keys only
         if (K > 0)
-            GSR_HIP(gsr_launch_col_pairs_scatter(perm, rect_sorted, f.P, d_valid,
+            GSR_HIP(gsr_launch_col_pairs_scatter(perm, rect_sorted,
+                                                 f.tight ? static_cast<const uint4 *>(ctx->rc_sorted.p)
+                                                         : nullptr,
+                                                 f.P, d_valid,
                                                  static_cast<const uint32_t *>(ctx->col_hist.p),
                                                  digit_total, f.col_shift, tv_alt, f.s),
                     "column scatter launch");
@@ -610,6 +631,8 @@ int forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings 
         GSR_HIP(hipMemsetAsync(ctx->ranges_local.p, 0, f.T_strip * 8, s), "hipMemsetAsync");
         out->num_rendered = 0;
         ctx->last_K = 0;
+        ctx->last_list = 0;
+        ctx->last_tight = false;
         ctx->last_gx = f.gx, ctx->last_gy = f.gy, ctx->last_rb = f.rb, ctx->last_re = f.re;
         ctx->last_point_list = static_cast<uint32_t *>(ctx->tile_vals.p);
         ctx->last_tiles_local = static_cast<uint32_t *>(ctx->tile_keys.p);
@@ -662,11 +685,13 @@ int forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings 
 
     out->num_rendered = (int64_t)f.K;
     ctx->last_K = (int64_t)f.K;
+    ctx->last_list = (int64_t)f.KL;
+    ctx->last_tight = f.tight;
     ctx->last_gx = f.gx, ctx->last_gy = f.gy, ctx->last_rb = f.rb, ctx->last_re = f.re;
     ctx->last_point_list = f.point_list;
     ctx->last_tiles_local = f.tiles_local;
     ctx->last_id_mask = f.id_mask;
-    ctx->last_packed = f.colpairs && f.K > 0;
+    ctx->last_packed = f.colpairs && f.KL > 0;
     ctx->have_forward = true;
     if (f.tmode) ++ctx->timed_frames;
     return GSR_OK;
@@ -740,7 +765,7 @@ void gsr_destroy(gsr_context *ctx) {
                       &ctx->rect_sorted, &ctx->pair_count,    &ctx->perm,       &ctx->ds_ctl,
                       &ctx->tile_keys,   &ctx->tile_vals,     &ctx->tile_keys_alt,
                       &ctx->tile_vals_alt, &ctx->ranges_local, &ctx->tile_diff, &ctx->col_hist,
-                      &ctx->color_ids, &ctx->blend_order};
+                      &ctx->color_ids, &ctx->blend_order, &ctx->strip_rc, &ctx->rc_sorted};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &set : ctx->ev)
@@ -774,6 +799,7 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
             ctx->fast = (int)value;
             return GSR_OK;
         case GSR_OPT_COLUMN_PAIRS: ctx->column_pairs = value ? 1 : 0; return GSR_OK;
+        case GSR_OPT_TIGHT_BINNING: ctx->tight = value ? 1 : 0; return GSR_OK;
         case GSR_OPT_COMPACT_SORT:
             if (value < -1 || value > 1) return fail(GSR_E_INVALID, "gsr_set_option: compact -1..1");
             ctx->compact_sort = (int)value;
@@ -831,8 +857,12 @@ int gsr_get_binning(gsr_context *ctx, uint32_t *point_list, uint32_t *point_tile
                     uint32_t *ranges, int64_t *num_rendered, int32_t *num_tiles, void *stream) {
     if (!ctx) return fail(GSR_E_INVALID, "gsr_get_binning: NULL context");
     if (!ctx->have_forward) return fail(GSR_E_STATE, "gsr_get_binning: no forward yet");
+    if (ctx->last_tight)
+        return fail(GSR_E_STATE, "gsr_get_binning: the last forward used tight binning (its lists "
+                                 "hold only the tiles each splat can reach); set "
+                                 "GSR_OPT_TIGHT_BINNING 0 or request n_contrib for upstream's lists");
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const int64_t K = ctx->last_K;
+    const int64_t K = ctx->last_list;
     const uint64_t T = (uint64_t)ctx->last_gx * ctx->last_gy;
     const uint64_t off = (uint64_t)ctx->last_rb * ctx->last_gx;
     const uint64_t T_strip = (uint64_t)ctx->last_gx * (ctx->last_re - ctx->last_rb);

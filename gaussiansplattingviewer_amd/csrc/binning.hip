@@ -342,11 +342,26 @@ static_assert(kCG == kRadixBins, "one thread per column in the column scans");
 
 struct ColScatterSmem {
     uint32_t x0w[kCG], y0h[kCG], id[kCG], seg0[kCG + 1];
+    uint32_t cols_lo[kCG], cols_hi[kCG];  // span words (tight binning, gsr::col_span)
     uint32_t colbase[kRadixBins], colw0[kRadixBins];
     uint32_t keys[kCSeg], vals[kCSeg];  // the round's segments by column
     uint32_t wpre[kCSeg + 1];           // pair offset of each sorted segment
     uint32_t tmp[4];
 };
+
+// Rows [lo, lo + cnt) (strip rect relative) of the segment of block Gaussian t in tile column
+// col.
+// (bit 31 of y0h: tight binning off, every rect full)
+__device__ __forceinline__ void seg_span(const ColScatterSmem &c, uint32_t t, uint32_t col,
+                                         uint32_t &lo, uint32_t &cnt) {
+    const uint2 rect = make_uint2(c.x0w[t], c.y0h[t] & 0x7FFFFFFFu);
+    if (c.y0h[t] >> 31) {
+        lo = 0u;
+        cnt = rect.y >> 16;
+        return;
+    }
+    col_span(rect, make_uint2(c.cols_lo[t], c.cols_hi[t]), col - (c.x0w[t] & 0xFFFFu), lo, cnt);
+}
 
 // One round of k_col_scatter: segments [R, R + rn) of the block, ranked kIt per lane (rn <=
 // 256 kIt; blocks with few segments take the smaller instantiation, whose ranking pass costs
@@ -370,8 +385,11 @@ __device__ __forceinline__ void col_round(uint32_t R, uint32_t rn, int pack_shif
                 if (c.seg0[mid] <= sg) lo = mid;
                 else hi = mid - 1;
             }
-            k[j] = (c.x0w[lo] & 0xFFFFu) + (sg - c.seg0[lo]);
-            v[j] = (uint32_t)lo;
+            const uint32_t col = (c.x0w[lo] & 0xFFFFu) + (sg - c.seg0[lo]);
+            uint32_t slo, sn;
+            seg_span(c, (uint32_t)lo, col, slo, sn);
+            k[j] = col;
+            v[j] = (uint32_t)lo | (slo << 8) | (sn << 12);  // Gaussian, its rows in the column
         }
     }
     radix_tile_scatter<kCW, kIt, false, false>(k, v, (int)rn, 0, 8, nullptr, 0, 0, nullptr,
@@ -381,7 +399,7 @@ __device__ __forceinline__ void col_round(uint32_t R, uint32_t rn, int pack_shif
 #pragma unroll
     for (int j = 0; j < kIt; ++j) {
         const uint32_t p = (uint32_t)(tid * kIt + j);
-        hh[j] = p < rn ? c.y0h[c.vals[p]] >> 16 : 0u;
+        hh[j] = p < rn ? c.vals[p] >> 12 : 0u;
         hsum += hh[j];
     }
     uint32_t npairs;
@@ -398,10 +416,10 @@ __device__ __forceinline__ void col_round(uint32_t R, uint32_t rn, int pack_shif
     // one thread per sorted segment (consecutive lanes: consecutive segments, so within a
     // column consecutive destination runs); each writes its h pairs
     for (uint32_t p = tid; p < rn; p += kCG) {
-        const uint32_t col = c.keys[p], t = c.vals[p];
-        const uint32_t y0h = c.y0h[t], id = c.id[t];
+        const uint32_t col = c.keys[p], v = c.vals[p], t = v & 0xFFu;
+        const uint32_t id = c.id[t];
         const uint32_t dst = c.colbase[col] + (c.wpre[p] - c.colw0[col]);
-        const uint32_t y0 = y0h & 0xFFFFu, h = y0h >> 16;
+        const uint32_t y0 = (c.y0h[t] & 0xFFFFu) + ((v >> 8) & 15u), h = v >> 12;
         for (uint32_t r = 0; r < h; ++r)
             out[dst + r] = (pack_shift < 32 ? (y0 + r) << pack_shift : 0u) | id;
     }
@@ -420,8 +438,10 @@ __device__ __forceinline__ void col_round(uint32_t R, uint32_t rn, int pack_shif
 constexpr int kCGroup = 4;
 __global__ __launch_bounds__(kCG) void k_col_count(const uint32_t *__restrict__ perm,
                                                    const uint2 *__restrict__ strip_rect,
+                                                   const uint4 *__restrict__ strip_rc,
                                                    const uint32_t *__restrict__ d_n,
                                                    uint2 *__restrict__ rect_sorted,
+                                                   uint4 *__restrict__ rc_sorted,
                                                    uint32_t *__restrict__ hist, int64_t ng,
                                                    uint32_t *__restrict__ off) {
     __shared__ uint32_t s_diff[kCGroup][kRadixBins + 1];
@@ -431,18 +451,38 @@ __global__ __launch_bounds__(kCG) void k_col_count(const uint32_t *__restrict__ 
     const int64_t base = (int64_t)blockIdx.x * (kCG * kCGroup);
     if (base >= n) return;  // whole group (k_rs_scan reads groups [0, ceil(n / 1024)) only)
     for (int i = tid; i < kCGroup * (kRadixBins + 1); i += kCG) (&s_diff[0][0])[i] = 0u;
-    uint2 r[kCGroup];
+    uint2 r[kCGroup], q[kCGroup];
 #pragma unroll
     for (int j = 0; j < kCGroup; ++j) {
         const int64_t e = base + j * kCG + tid;
-        r[j] = e < n ? strip_rect[perm[e]] : make_uint2(0u, 0u);
-        if (e < n) rect_sorted[e] = r[j];
+        const uint32_t id = e < n ? perm[e] : 0u;
+        r[j] = q[j] = make_uint2(0u, 0u);
+        if (e < n && strip_rc) {  // tight binning: the rect and its span word, one 16-B gather
+            const uint4 rq = strip_rc[id];
+            r[j] = make_uint2(rq.x, rq.y);
+            q[j] = make_uint2(rq.z, rq.w);
+            rc_sorted[e] = rq;
+        } else if (e < n) {
+            r[j] = strip_rect[id];
+            rect_sorted[e] = r[j];
+        }
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kCGroup; ++j) {
         const uint32_t x0 = r[j].x & 0xFFFFu, w = r[j].x >> 16, h = r[j].y >> 16;
-        if (w) {
+        if (w && strip_rc && span_coded(r[j])) {
+            // column c holds cnt_c pairs: the difference cnt_c - cnt_{c-1} at column x0 + c
+            uint32_t prev = 0u;
+#pragma unroll
+            for (uint32_t c = 0; c <= kSpanCols; ++c) {
+                if (c > w) break;
+                uint32_t lo, cnt = 0u;
+                if (c < w) col_span(r[j], q[j], c, lo, cnt);
+                if (cnt != prev) atomicAdd(&s_diff[j][x0 + c], cnt - prev);
+                prev = cnt;
+            }
+        } else if (w) {
             atomicAdd(&s_diff[j][x0], h);
             atomicAdd(&s_diff[j][x0 + w], 0u - h);
         }
@@ -463,6 +503,7 @@ __global__ __launch_bounds__(kCG) void k_col_count(const uint32_t *__restrict__ 
 
 __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict__ perm,
                                                      const uint2 *__restrict__ rect_sorted,
+                                                     const uint4 *__restrict__ rc_sorted,
                                                      const uint32_t *__restrict__ d_n,
                                                      const uint32_t *__restrict__ hist, int64_t ng,
                                                      const uint32_t *__restrict__ off,
@@ -479,9 +520,18 @@ __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict_
     if (base >= n) return;
     const int64_t e = base + tid;
     const bool valid = e < n;
-    const uint2 r = valid ? rect_sorted[e] : make_uint2(0u, 0u);
+    uint2 r = make_uint2(0u, 0u), q = r;
+    if (valid && rc_sorted) {
+        const uint4 rq = rc_sorted[e];
+        r = make_uint2(rq.x, rq.y);
+        q = make_uint2(rq.z, rq.w);
+    } else if (valid) {
+        r = rect_sorted[e];
+    }
     c.x0w[tid] = r.x;
-    c.y0h[tid] = r.y;
+    c.y0h[tid] = rc_sorted ? r.y : (r.y | 0x80000000u);  // bit 31: not span-coded (full)
+    c.cols_lo[tid] = q.x;
+    c.cols_hi[tid] = q.y;
     c.id[tid] = valid ? perm[e] : 0u;
     uint32_t tot;
     // global start of column d for this block: all earlier columns, then earlier blocks
@@ -634,48 +684,78 @@ namespace {
 // [start_t, start_t + count_t) with start_t the exclusive scan of the per-tile pair counts --
 // which depend only on the Gaussians' tile rects, not on any sort.  They are computed on the
 // second stream while the main stream sorts, in two kernels:
-//   k_tile_diff     -- per block of Gaussians, in LDS: for every tile row y of a rect, a 1D
-//                      difference array over the columns (+1 at x0, -1 at x1), and one over the
-//                      rows of the rect widths (+w at y0, -w at y1); the block's arrays go to
-//                      `partial` (kTileDiffBlocks of them);
-//   k_tile_finalize -- one block per tile row: sums the partials of its row, prefix over x =
-//                      the row's per-tile counts; the row's first offset = the sum of the pair
-//                      counts of the rows above (prefix of the row-width differences, then a
-//                      prefix of those row totals); then an exclusive scan along the row.
+//   k_tile_diff     -- per block of Gaussians, in LDS: for every tile column of a rect (or of
+//                      its tight spans), a difference array down the rows (+1 at the first row,
+//                      -1 past the last: two LDS atomics per column), then per column the prefix
+//                      down the rows = the block's per-tile counts, and the rows' totals; the
+//                      block's counts and totals go to `partial` (kTileDiffBlocks of them);
+//   k_tile_finalize -- one block per tile row: sums the partials' counts of its row; the row's
+//                      first offset = the sum of the row totals above; then an exclusive scan
+//                      along the row.
 // Tiles without pairs get (0, 0), as upstream's memset leaves them.  Replaces k_ranges, a pass
 // over the K sorted keys on the main stream (the packed pair list has no tile keys to scan).
 constexpr int kDiffThreads = 1024;
 
 __global__ __launch_bounds__(kDiffThreads) void k_tile_diff(const uint2 *__restrict__ strip_rect,
+                                                            const uint4 *__restrict__ strip_rc,
                                                             int64_t P, uint32_t gx, uint32_t rows,
                                                             uint32_t *__restrict__ partial) {
     extern __shared__ uint32_t s_diff[];
     const uint32_t w1 = gx + 1, cells = gsr_tile_diff_cells(gx, rows);
-    uint32_t *s_rows = s_diff + w1 * rows;  // rows + 1 row-width differences
+    uint32_t *s_rows = s_diff + w1 * (rows + 1);  // the rows' pair totals
     for (uint32_t c = threadIdx.x; c < cells; c += kDiffThreads) s_diff[c] = 0u;
     __syncthreads();
     const int64_t b0 = P * blockIdx.x / gridDim.x, b1 = P * (blockIdx.x + 1) / gridDim.x;
     // 4 rects per thread and step, their loads issued together
     constexpr int kU = 4;
     for (int64_t i = b0 + threadIdx.x; i < b1; i += kU * kDiffThreads) {
-        uint2 r[kU];
+        uint2 r[kU], q[kU];
 #pragma unroll
         for (int k = 0; k < kU; ++k) {
             const int64_t j = i + (int64_t)k * kDiffThreads;
-            r[k] = j < b1 ? strip_rect[j] : make_uint2(0u, 0u);
+            r[k] = q[k] = make_uint2(0u, 0u);
+            if (j < b1 && strip_rc) {
+                const uint4 rq = strip_rc[j];
+                r[k] = make_uint2(rq.x, rq.y);
+                q[k] = make_uint2(rq.z, rq.w);
+            } else if (j < b1) {
+                r[k] = strip_rect[j];
+            }
         }
 #pragma unroll
         for (int k = 0; k < kU; ++k) {
             if (r[k].x == 0u) continue;  // no pairs in the strip (a rect with pairs has width > 0)
-            const uint32_t x0 = r[k].x & 0xFFFFu, w = r[k].x >> 16;
-            const uint32_t y0 = r[k].y & 0xFFFFu, y1 = y0 + (r[k].y >> 16);
-            for (uint32_t y = y0; y < y1; ++y) {
-                atomicAdd(&s_diff[y * w1 + x0], 1u);
-                atomicAdd(&s_diff[y * w1 + x0 + w], 0xFFFFFFFFu);  // -1 (mod 2^32)
+            const uint32_t x0 = r[k].x & 0xFFFFu, w = r[k].x >> 16, y0 = r[k].y & 0xFFFFu;
+            const bool coded = strip_rc && span_coded(r[k]);
+            // column x0 + c holds rows [y0 + lo, y0 + lo + cnt): +1 / -1 down the column
+            for (uint32_t c = 0; c < w; ++c) {
+                uint32_t lo = 0u, cnt = r[k].y >> 16;
+                if (coded) col_span(r[k], q[k], c, lo, cnt);
+                if (cnt) {
+                    atomicAdd(&s_diff[(y0 + lo) * w1 + x0 + c], 1u);
+                    atomicAdd(&s_diff[(y0 + lo + cnt) * w1 + x0 + c], 0xFFFFFFFFu);  // -1
+                }
             }
-            atomicAdd(&s_rows[y0], w);
-            atomicAdd(&s_rows[y1], 0u - w);
         }
+    }
+    __syncthreads();
+    // per column, the prefix down the rows: each tile's pair count (in place)
+    for (uint32_t x = threadIdx.x; x < gx; x += kDiffThreads) {
+        uint32_t run = 0u;
+        for (uint32_t y = 0; y < rows; ++y) {
+            run += s_diff[y * w1 + x];
+            s_diff[y * w1 + x] = run;
+        }
+    }
+    __syncthreads();
+    // the rows' totals
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    for (uint32_t y = wv; y < rows; y += kDiffThreads / 64) {
+        uint32_t acc = 0u;
+        for (uint32_t x = ln; x < gx; x += 64) acc += s_diff[y * w1 + x];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        if (ln == 0) s_rows[y] = acc;
     }
     __syncthreads();
     uint32_t *dst = partial + (int64_t)blockIdx.x * cells;
@@ -698,37 +778,27 @@ __global__ __launch_bounds__(kFinThreads) void k_tile_finalize(const uint32_t *_
     __shared__ uint32_t s_tmp[kW];
     const uint32_t y = blockIdx.x, w1 = gx + 1, cells = gsr_tile_diff_cells(gx, rows);
     const int tid = threadIdx.x;
-    // offset of this row: sum over rows y' < y of rowtotal[y'] = prefix of the width differences
+    // offset of this row: the sum of the row totals above it
     uint32_t before = 0;
-    {
-        uint32_t carry_rd = 0, carry_tot = 0;
-        for (uint32_t y0 = 0; y0 < y; y0 += kFinThreads) {
-            const uint32_t yy = y0 + tid;
-            uint32_t rd = 0;
-            if (yy < y)
+    for (uint32_t y0 = 0; y0 < y; y0 += kFinThreads) {
+        const uint32_t yy = y0 + tid;
+        uint32_t rt = 0;
+        if (yy < y)
 #pragma unroll 8
-                for (int b = 0; b < nparts; ++b) rd += partial[(int64_t)b * cells + w1 * rows + yy];
-            uint32_t t1, t2;
-            const uint32_t rowtotal = blockw_inclusive_scan<kW>(rd, s_tmp, t1) + carry_rd;
-            carry_rd += t1;
-            const uint32_t sum = blockw_inclusive_scan<kW>(yy < y ? rowtotal : 0u, s_tmp, t2);
-            (void)sum;
-            carry_tot += t2;
-        }
-        before = carry_tot;
+            for (int b = 0; b < nparts; ++b) rt += partial[(int64_t)b * cells + w1 * (rows + 1) + yy];
+        uint32_t t;
+        blockw_inclusive_scan<kW>(rt, s_tmp, t);
+        before += t;
     }
-    // this row's counts: prefix over x of the summed column differences, then an exclusive
-    // scan along the row
-    uint32_t carry_d = 0, start = before;
+    // this row's counts (the partials' sum), then an exclusive scan along the row
+    uint32_t start = before;
     for (uint32_t x0 = 0; x0 < gx; x0 += kFinThreads) {
         const uint32_t x = x0 + tid;
-        uint32_t d = 0;
+        uint32_t cnt = 0;
         if (x < gx)
 #pragma unroll 8
-            for (int b = 0; b < nparts; ++b) d += partial[(int64_t)b * cells + y * w1 + x];
-        uint32_t t1, t2;
-        const uint32_t cnt = blockw_inclusive_scan<kW>(d, s_tmp, t1) + carry_d;
-        carry_d += t1;
+            for (int b = 0; b < nparts; ++b) cnt += partial[(int64_t)b * cells + y * w1 + x];
+        uint32_t t2;
         const uint32_t ex = blockw_exclusive_scan<kW>(x < gx ? cnt : 0u, s_tmp, t2) + start;
         start += t2;
         if (x < gx) ranges[y * gx + x] = cnt ? make_uint2(ex, ex + cnt) : make_uint2(0u, 0u);
@@ -737,8 +807,8 @@ __global__ __launch_bounds__(kFinThreads) void k_tile_finalize(const uint32_t *_
 
 }  // namespace
 
-hipError_t gsr_launch_tile_ranges_aux(const uint2 *strip_rect, int64_t P, uint32_t gx,
-                                      uint32_t rows, uint32_t *partial, uint2 *ranges,
+hipError_t gsr_launch_tile_ranges_aux(const uint2 *strip_rect, const uint4 *strip_rc, int64_t P,
+                                      uint32_t gx, uint32_t rows, uint32_t *partial, uint2 *ranges,
                                       hipStream_t s) {
     const uint32_t cells = gsr_tile_diff_cells(gx, rows);
     const size_t lds = (size_t)cells * 4;
@@ -759,8 +829,8 @@ hipError_t gsr_launch_tile_ranges_aux(const uint2 *strip_rect, int64_t P, uint32
     // one block per 16k rects (at least 64, at most kTileDiffBlocks): the rect pass stays
     // short at 6M Gaussians while the finalize's sum over the partials stays small at 1M
     const int nparts = (int)std::min<int64_t>(kTileDiffBlocks, std::max<int64_t>(64, (P + 16383) / 16384));
-    hipLaunchKernelGGL(k_tile_diff, dim3(nparts), dim3(kDiffThreads), lds, s, strip_rect, P, gx,
-                       rows, partial);
+    hipLaunchKernelGGL(k_tile_diff, dim3(nparts), dim3(kDiffThreads), lds, s, strip_rect,
+                       strip_rc, P, gx, rows, partial);
     hipLaunchKernelGGL(k_tile_finalize, dim3(rows), dim3(kFinThreads), 0, s, partial,
                        nparts, gx, rows, ranges);
     return hipGetLastError();
@@ -811,25 +881,27 @@ int64_t gsr_col_blocks(int64_t n) {
     return nb + ng;
 }
 
-hipError_t gsr_launch_col_pairs_count(const uint32_t *perm, const uint2 *strip_rect, int64_t n_max,
-                                      const uint32_t *d_n, uint2 *rect_sorted, uint32_t *hist,
+hipError_t gsr_launch_col_pairs_count(const uint32_t *perm, const uint2 *strip_rect,
+                                      const uint4 *strip_rc, int64_t n_max, const uint32_t *d_n,
+                                      uint2 *rect_sorted, uint4 *rc_sorted, uint32_t *hist,
                                       uint32_t *digit_total, hipStream_t s) {
     const int64_t nb = (n_max + kCG - 1) / kCG, ng = (nb + kCGroup - 1) / kCGroup;
     if (nb == 0) return hipSuccess;
     uint32_t *off = hist + ng * kRadixBins;
-    hipLaunchKernelGGL(k_col_count, dim3((unsigned)ng), dim3(kCG), 0, s, perm, strip_rect, d_n,
-                       rect_sorted, hist, ng, off);
+    hipLaunchKernelGGL(k_col_count, dim3((unsigned)ng), dim3(kCG), 0, s, perm, strip_rect,
+                       strip_rc, d_n, rect_sorted, rc_sorted, hist, ng, off);
     return gsr_launch_digit_scan_n(hist, ng, digit_total, d_n, kCG * kCGroup, s);
 }
 
 hipError_t gsr_launch_col_pairs_scatter(const uint32_t *perm, const uint2 *rect_sorted,
-                                        int64_t n_max, const uint32_t *d_n, const uint32_t *hist,
+                                        const uint4 *rc_sorted, int64_t n_max,
+                                        const uint32_t *d_n, const uint32_t *hist,
                                         const uint32_t *digit_total, int pack_shift, uint32_t *out,
                                         hipStream_t s) {
     const int64_t nb = (n_max + kCG - 1) / kCG, ng = (nb + kCGroup - 1) / kCGroup;
     if (nb == 0) return hipSuccess;
     const uint32_t *off = hist + ng * kRadixBins;
-    hipLaunchKernelGGL(k_col_scatter, dim3((unsigned)nb), dim3(kCG), 0, s, perm, rect_sorted, d_n,
-                       hist, ng, off, digit_total, pack_shift, out);
+    hipLaunchKernelGGL(k_col_scatter, dim3((unsigned)nb), dim3(kCG), 0, s, perm, rect_sorted,
+                       rc_sorted, d_n, hist, ng, off, digit_total, pack_shift, out);
     return hipGetLastError();
 }

@@ -161,6 +161,31 @@ __device__ __forceinline__ uint32_t float_sort_key(float f) {
     return u;
 }
 
+// --- tight binning: the tile rows each column of a splat's rect really reaches ------------
+// Upstream pairs a Gaussian with every tile of its 3-sigma square (getRect); at C3 ~43 % of those
+// tiles lie outside the ellipse where the splat can reach alpha >= 1/255, and the blend skips them
+// there (upstream `alpha < 1/255: continue`).  A Gaussian whose strip rect has w <= kSpanCols
+// columns and h <= kSpanRows rows carries a span word: byte c = lo | cnt << 4, the strip rect's
+// rows [lo, lo + cnt) that column c of the rect keeps (preprocess.hip col_spans).  Tight binning
+// (GSR_OPT_TIGHT_BINNING) emits only those pairs; every tile list keeps its order, so each
+// pixel composites exactly the same splats in the same order.  Larger rects keep every tile.
+constexpr uint32_t kSpanCols = 8, kSpanRows = 15;
+__device__ __forceinline__ bool span_coded(uint2 rect) {
+    return (rect.x >> 16) <= kSpanCols && (rect.y >> 16) <= kSpanRows;
+}
+// Rows [lo, lo + cnt) of column c (< width) of the rect; cols is ignored unless span_coded.
+__device__ __forceinline__ void col_span(uint2 rect, uint2 cols, uint32_t c, uint32_t &lo,
+                                         uint32_t &cnt) {
+    if (span_coded(rect)) {
+        const uint32_t b = ((c < 4 ? cols.x : cols.y) >> (8 * (c & 3))) & 0xFFu;
+        lo = b & 15u;
+        cnt = b >> 4;
+    } else {
+        lo = 0u;
+        cnt = rect.y >> 16;
+    }
+}
+
 // --- wave / block scans (256-thread blocks, wave64) ------------------------------------
 __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
     const int lane = threadIdx.x & 63;
@@ -215,10 +240,15 @@ struct GsrPreprocessArgs {
     // per Gaussian: strip-clipped tile rect {x0 | width << 16, strip-local row0 | rows << 16},
     // {0, 0} when it has no pair in the strip (grid dimensions < 2^16, checked by the host)
     uint2 *strip_rect;
-    // per k_preprocess block (ceil(P / 256)): its (Gaussian, strip tile) pair count, then as
-    // many uint2 of the OR / AND of its kept depth keys
+    // tight binning (else NULL): per Gaussian {strip rect, span word} (gsr::col_span; the span
+    // word is read only for span-coded rects), {0, 0, 0, 0} without pairs in the strip
+    uint4 *strip_rc;
+    // per k_preprocess block (ceil(P / 256)): its (Gaussian, strip tile) pair count (low 32
+    // bits) and its pair count over the spans (high 32 bits: the same without tight binning),
+    // then as many uint2 of the OR / AND of its kept depth keys
     uint64_t *block_pairs;
-    unsigned long long *host_K;  // pinned host memory (device-mapped): [K, D, -, -, -, K tag]
+    // pinned host memory (device-mapped): [K, D, -, K over the spans, -, K tag]
+    unsigned long long *host_K;
     uint32_t k_tag;              // nonzero: stored to host_K[5] after K (the host spins on it)
     // optional debug outputs
     float *depths, *means2D, *conic_opacity, *rgb;
@@ -234,8 +264,8 @@ hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int waves_per_simd, hipS
 bool gsr_color_ids_ok(const GsrPreprocessArgs &a);
 hipError_t gsr_launch_color_ids(const GsrPreprocessArgs &a, const uint32_t *ids,
                                 const uint32_t *d_n, int waves_per_simd, hipStream_t s);
-// K of the frame (sum of the preprocess blocks' pair counts) and D -> a.host_K (pinned host
-// memory), after the preprocess.
+// K of the frame (sum of the preprocess blocks' pair counts), the pair count over the spans and
+// D -> a.host_K (pinned host memory), after the preprocess.
 hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s);
 hipError_t gsr_launch_mark_visible(const float *means3D, int64_t P, const float *viewmatrix,
                                    uint8_t *visible, hipStream_t s);
@@ -329,11 +359,15 @@ hipError_t gsr_launch_dup_sort_pass(const uint4 *bin, const uint32_t *chunk_firs
 // segments of the depth-sorted Gaussians.  hist: gsr_col_blocks(n_max) * 256 words (per group of
 // 4 blocks its column totals, per block its offsets within the group).
 int64_t gsr_col_blocks(int64_t n);
-hipError_t gsr_launch_col_pairs_count(const uint32_t *perm, const uint2 *strip_rect, int64_t n_max,
-                                      const uint32_t *d_n, uint2 *rect_sorted, uint32_t *hist,
+// Tight binning: strip_rc (GsrPreprocessArgs) instead of strip_rect, and the depth-ordered copy
+// goes to rc_sorted instead of rect_sorted (NULL: full rects).
+hipError_t gsr_launch_col_pairs_count(const uint32_t *perm, const uint2 *strip_rect,
+                                      const uint4 *strip_rc, int64_t n_max, const uint32_t *d_n,
+                                      uint2 *rect_sorted, uint4 *rc_sorted, uint32_t *hist,
                                       uint32_t *digit_total, hipStream_t s);
 hipError_t gsr_launch_col_pairs_scatter(const uint32_t *perm, const uint2 *rect_sorted,
-                                        int64_t n_max, const uint32_t *d_n, const uint32_t *hist,
+                                        const uint4 *rc_sorted, int64_t n_max,
+                                        const uint32_t *d_n, const uint32_t *hist,
                                         const uint32_t *digit_total, int pack_shift, uint32_t *out,
                                         hipStream_t s);
 hipError_t gsr_launch_digit_scan_n(uint32_t *hist, int64_t nb, uint32_t *digit_total,
@@ -352,11 +386,13 @@ hipError_t gsr_launch_ranges(const uint32_t *tile_keys, int64_t K, uint32_t *ran
 // (the difference arrays live in LDS).
 constexpr int kTileDiffBlocks = 256;  // at most; 64 up to 1M Gaussians, more for more
 constexpr uint32_t kTileDiffMaxCells = 38912;  // 152 KiB of LDS
-// (gx + 1) column-difference cells per tile row, then rows + 1 row-width differences
+// (gx + 1) cells per tile row for rows + 1 rows (the column differences, then the per-tile
+// counts), then the rows' pair totals
 __host__ __device__ inline uint32_t gsr_tile_diff_cells(uint32_t gx, uint32_t rows) {
-    return (gx + 1) * rows + rows + 1;
+    return (gx + 1) * (rows + 1) + rows;
 }
-hipError_t gsr_launch_tile_ranges_aux(const uint2 *strip_rect, int64_t P, uint32_t gx,
+hipError_t gsr_launch_tile_ranges_aux(const uint2 *strip_rect, const uint4 *strip_rc, int64_t P,
+                                      uint32_t gx,
                                       uint32_t rows, uint32_t *partial, uint2 *ranges,
                                       hipStream_t s);
 // Pair count per tile row of a strip's ranges (gsr_tile_row_pairs).

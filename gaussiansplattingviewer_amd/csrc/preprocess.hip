@@ -192,6 +192,60 @@ __device__ __forceinline__ float3 cull_data(float A, float B, float C, float o) 
     return make_float3(ex, ey, __uint_as_float(__float_as_uint(Lm) + 1u));
 }
 
+// Span word of a span-coded strip rect (gsr_internal.h col_span): per column of the rect, the
+// tile rows whose pixel-centre box meets the ellipse q(d) = A dx^2 + 2B dx dy + C dy^2 <= 2 Lm
+// (cull_data's region, which holds every pixel where the blend can reach alpha >= 1/255),
+// widened outward.  Over a column's pixel-centre range dx in [ua, ub] the ellipse's dy extent is
+// reached at the column's edges or, if it lies inside, at the ellipse's top / bottom point.
+// Returns the pair count over the spans.  x0 / w: the rect's tile columns; sy0 / h: its
+// strip-clipped global tile rows.
+__device__ __forceinline__ uint32_t col_spans(float px, float py, float A, float B, float C,
+                                              float Lm, uint32_t x0, uint32_t w, uint32_t sy0,
+                                              uint32_t h, uint2 &cols) {
+    uint64_t word = 0;
+    for (uint32_t c = 0; c < w; ++c) word |= (uint64_t)(h << 4) << (8 * c);
+    cols = make_uint2((uint32_t)word, (uint32_t)(word >> 32));
+    // the determinant in double (A C ~ B^2 for elongated splats), the rest in float with the
+    // hardware reciprocal / square root (1 ulp): their rounding (~1e-6 relative, ~1e-3 of vmax
+    // where the square root's argument cancels at the ellipse's u extremes) sits inside the
+    // margins (1e-5 on the threshold, 2e-3 vmax + 0.02 px on the extents)
+    const double det_d = (double)A * (double)C - (double)B * (double)B;
+    if (!(det_d > 0.0) || !(A > 0.0f) || !(C > 0.0f) || !(Lm < 1e30f) || !(fabsf(px) < 1e30f) ||
+        !(fabsf(py) < 1e30f))
+        return w * h;
+    const float det = (float)det_d, idet = __builtin_amdgcn_rcpf(det);
+    const float T2 = 2.0f * Lm * (1.0f + 1e-5f) + 1e-5f;
+    const float vmax = __builtin_amdgcn_sqrtf(A * T2 * idet);
+    const float umax = __builtin_amdgcn_sqrtf(C * T2 * idet) * (1.0f + 1e-5f) + 0.02f;
+    if (!(vmax < 1e30f) || !(umax < 1e30f) || !(det > 0.0f)) return w * h;
+    const float ut = -B * vmax * __builtin_amdgcn_rcpf(A), ev = 2e-3f * vmax + 0.02f;
+    const float rc = __builtin_amdgcn_rcpf(C), cT2 = C * T2;
+    // rows relative to the rect: [lo, hi] clamped to [0, h - 1]
+    const float ylo = py - ev - 15.0f - 16.0f * (float)sy0, yhi = py + ev - 16.0f * (float)sy0;
+    const float hmax = (float)(h - 1);
+    word = 0;
+    uint32_t pairs = 0;
+#pragma unroll 1
+    for (uint32_t c = 0; c < w; ++c) {
+        const float cx = 16.0f * (float)(x0 + c);
+        const float ua = fmaxf(cx - px, -umax), ub = fminf(cx + 15.0f - px, umax);
+        if (!(ua <= ub)) continue;
+        const float ha = __builtin_amdgcn_sqrtf(fmaxf(0.0f, cT2 - det * ua * ua));
+        const float hb = __builtin_amdgcn_sqrtf(fmaxf(0.0f, cT2 - det * ub * ub));
+        const float vhi = (ut >= ua && ut <= ub) ? vmax : fmaxf(-B * ua + ha, -B * ub + hb) * rc;
+        const float vlo = (-ut >= ua && -ut <= ub) ? -vmax : fminf(-B * ua - ha, -B * ub - hb) * rc;
+        const float lo = fmaxf(ceilf((ylo + vlo) * 0.0625f), 0.0f);
+        const float hi = fminf(floorf((yhi + vhi) * 0.0625f), hmax);
+        if (lo <= hi) {
+            const uint32_t l = (uint32_t)lo, n = (uint32_t)(hi - lo) + 1u;
+            word |= (uint64_t)(l | (n << 4)) << (8 * c);
+            pairs += n;
+        }
+    }
+    cols = make_uint2((uint32_t)word, (uint32_t)(word >> 32));
+    return pairs;
+}
+
 // Strip ranks without radii (strip_skip): may the Gaussian at view-space t with 3D covariance
 // c[6] and pixel row py have a tile in the strip?  False only when provably not: from an upper
 // bound of upstream's radius ceil(3 sqrt(lambda_max)) -- lambda_max of the 2D covariance
@@ -267,14 +321,19 @@ __device__ __forceinline__ Front front_one(const GsrPreprocessArgs &a, int64_t i
 // per-Gaussian extras are not requested).
 __device__ __forceinline__ void none_one(const GsrPreprocessArgs &a, int64_t idx) {
     a.strip_rect[idx] = make_uint2(0u, 0u);
+    if (a.strip_rc) a.strip_rc[idx] = make_uint4(0u, 0u, 0u, 0u);
     a.sort_keys[idx] = 0xFFFFFFFFu;
 }
 
-// The second half: 2D covariance, conic, radius, tile rect, depth key, the blend's record.
-// Returns the number of (Gaussian, strip tile) pairs of Gaussian idx.
+// The second half: 2D covariance, conic, radius, tile rect, depth key, the blend's record (and
+// with tight binning the span word).  Returns the number of (Gaussian, strip tile) pairs of
+// Gaussian idx; tight_out: their number over the spans (without tight binning the same).
 __device__ __forceinline__ uint32_t back_one(const GsrPreprocessArgs &a, int64_t idx,
-                                             const Front &f, uint32_t &key_out) {
+                                             const Front &f, uint32_t &key_out,
+                                             uint32_t &tight_out) {
     int32_t radius_out = 0;
+    uint32_t strip_tiles_tight = 0;
+    uint2 cols = make_uint2(0u, 0u);
     uint32_t strip_tiles = 0, all_tiles = 0;
     uint2 strip_rect = make_uint2(0u, 0u);
     uint32_t key = 0xFFFFFFFFu;
@@ -312,6 +371,9 @@ __device__ __forceinline__ uint32_t back_one(const GsrPreprocessArgs &a, int64_t
                     cd = cull_data(conic_a, conic_b, conic_c, opacity);
                     rec.a = make_float4(px, py, conic_a, conic_b);
                     rec.b = make_float4(conic_c, opacity, cd.x, cd.y);
+                    if (a.strip_rc && span_coded(strip_rect))
+                        strip_tiles_tight = col_spans(px, py, conic_a, conic_b, conic_c, cd.z,
+                                                      rc.x0, rc.x1 - rc.x0, sy0, sy1 - sy0, cols);
                 }
                 if (strip_tiles) rec.c.x = cd.z;  // c.yzw: the colour, written by k_color
                 if (a.depths) a.depths[idx] = p_view.z;
@@ -327,6 +389,9 @@ __device__ __forceinline__ uint32_t back_one(const GsrPreprocessArgs &a, int64_t
     }
     if (a.radii) a.radii[idx] = radius_out;
     a.strip_rect[idx] = strip_rect;
+    if (a.strip_rc) a.strip_rc[idx] = make_uint4(strip_rect.x, strip_rect.y, cols.x, cols.y);
+    tight_out =
+        (strip_rect.x && a.strip_rc && span_coded(strip_rect)) ? strip_tiles_tight : strip_tiles;
     a.sort_keys[idx] = key;  // the depth sort's values are the indices (implicit)
     key_out = key;
     if (a.tiles_touched) a.tiles_touched[idx] = strip_tiles;
@@ -351,9 +416,9 @@ template <bool kSkip>
 __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t key = 0xFFFFFFFFu;
-    uint32_t pairs = 0u;
+    uint32_t pairs = 0u, tight = 0u;
     if (!kSkip) {
-        if (idx < a.P) pairs = back_one(a, idx, front_one(a, idx), key);
+        if (idx < a.P) pairs = back_one(a, idx, front_one(a, idx), key, tight);
     } else {
         __shared__ SkipSmem sk;
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -398,7 +463,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
             for (int i = 0; i < 6; ++i) g.cov3d[i] = sk.v[5 + i][t];
             g.opacity = sk.v[11][t];
             g.in_frustum = true;
-            pairs = back_one(a, (int64_t)sk.idx[t], g, key);
+            pairs = back_one(a, (int64_t)sk.idx[t], g, key, tight);
         }
     }
     const bool kept = pairs != 0u;  // has pairs in the strip <=> its depth key is kept
@@ -406,18 +471,21 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         v += __shfl_xor(v, off);
+        tight += __shfl_xor(tight, off);
         o |= __shfl_xor(o, off);
         an &= __shfl_xor(an, off);
     }
-    __shared__ uint32_t s_red[4][4];
+    __shared__ uint32_t s_red[5][4];
     const uint32_t c = a.block_kept ? (uint32_t)__popcll(__ballot(kept)) : 0u;
     if ((threadIdx.x & 63) == 0) {
         const int w = threadIdx.x >> 6;
-        s_red[0][w] = v, s_red[1][w] = o, s_red[2][w] = an, s_red[3][w] = c;
+        s_red[0][w] = v, s_red[1][w] = o, s_red[2][w] = an, s_red[3][w] = c, s_red[4][w] = tight;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        a.block_pairs[blockIdx.x] = (uint64_t)s_red[0][0] + s_red[0][1] + s_red[0][2] + s_red[0][3];
+        a.block_pairs[blockIdx.x] =
+            ((uint64_t)(s_red[4][0] + s_red[4][1] + s_red[4][2] + s_red[4][3]) << 32) |
+            (s_red[0][0] + s_red[0][1] + s_red[0][2] + s_red[0][3]);
         reinterpret_cast<uint2 *>(a.block_pairs + gridDim.x)[blockIdx.x] =
             make_uint2(s_red[1][0] | s_red[1][1] | s_red[1][2] | s_red[1][3],
                        s_red[2][0] & s_red[2][1] & s_red[2][2] & s_red[2][3]);
@@ -429,14 +497,15 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
 // visible): K = sum of the per-block pair counts and D = the bits in which the kept depth keys
 // differ (bits of OR ^ AND: the depth sort's pass count), stored straight into pinned host
 // memory (system scope) so the host can read them as soon as this kernel's completion event
-// fires -- no copy, and nothing added to the main stream.  host_K[0] = K, host_K[1] = D.
+// fires -- no copy, and nothing added to the main stream.  host_K[0] = K, host_K[1] = D,
+// host_K[3] = the pair count over the spans (the high halves of the block counts).
 __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__restrict__ cnt,
                                                     const uint2 *__restrict__ keybits, int64_t n,
                                                     unsigned long long *host_K,
                                                     uint32_t k_tag) {
-    __shared__ unsigned long long s_w[16];
+    __shared__ unsigned long long s_w[16], s_wt[16];
     __shared__ uint32_t s_or[16], s_and[16];
-    unsigned long long v = 0;
+    unsigned long long v = 0, vt = 0;
     uint32_t o = 0u, a = 0xFFFFFFFFu;
     // 8 blocks' entries per thread and round, their loads in flight together (one dependent
     // load per 1024 blocks took 23 us at 6M Gaussians)
@@ -452,7 +521,8 @@ __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            v += c[u];
+            v += c[u] & 0xFFFFFFFFull;
+            vt += c[u] >> 32;
             o |= kb[u].x;
             a &= kb[u].y;
         }
@@ -460,27 +530,31 @@ __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         v += __shfl_xor(v, off);
+        vt += __shfl_xor(vt, off);
         o |= __shfl_xor(o, off);
         a &= __shfl_xor(a, off);
     }
     if ((threadIdx.x & 63) == 0) {
         s_w[threadIdx.x >> 6] = v;
+        s_wt[threadIdx.x >> 6] = vt;
         s_or[threadIdx.x >> 6] = o;
         s_and[threadIdx.x >> 6] = a;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned long long t = 0;
+        unsigned long long t = 0, tt = 0;
         o = 0u;
         a = 0xFFFFFFFFu;
         for (int i = 0; i < 16; ++i) {
             t += s_w[i];
+            tt += s_wt[i];
             o |= s_or[i];
             a &= s_and[i];
         }
         const uint32_t diff = t ? (o ^ a) : 0u;
         const unsigned long long D = diff ? 32u - (uint32_t)__clz(diff) : 0u;
         __hip_atomic_store(host_K + 1, D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_K + 3, tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(host_K, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         // the host spins on this tag instead of sleeping in an event wait (release: K and D are
         // visible first)

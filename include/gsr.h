@@ -200,8 +200,8 @@ int gsr_set_timing(gsr_context *ctx, int enable);
 int gsr_stage_times(gsr_context *ctx, float *ms, int n);
 const char *gsr_stage_name(int i);
 
-/* Options (per context; every setting renders the same binning, and the blend options change
- * pixels by float rounding at most -- tests/test_gpu_parity.py checks each):
+/* Options (per context; every setting renders the same image bits except the blend arithmetic,
+ * which changes pixels by float rounding at most -- tests/test_gpu_parity.py checks each):
  *   GSR_OPT_BLEND_CULL (default 1): conservative ellipse-vs-quadrant cull in the blend;
  *     outputs are bit-identical either way.
  *   GSR_OPT_BLEND_FAST (default 1): blend arithmetic with log2(e) folded into the conic, FMA
@@ -215,9 +215,15 @@ const char *gsr_stage_name(int i);
  *   GSR_OPT_COMPACT_SORT (default -1 = auto): 1 = the depth sort first compacts the keys of the
  *     Gaussians with pairs in the strip and sorts only those; 0 = its first pass drops the others
  *     while it sorts; auto = compact on strips (a proper subset of the tile rows) of >= 4M
- *     Gaussians. */
+ *     Gaussians.
+ *   GSR_OPT_TIGHT_BINNING (default 1): with the column-first form and no n_contrib output, each
+ *     Gaussian of a rect up to 8 tile columns x 15 rows is paired only with the tiles its
+ *     alpha >= 1/255 ellipse reaches (upstream's blend skips it on the others), so the lists are
+ *     subsequences of upstream's and every pixel composites the same splats in the same order.
+ *     num_rendered stays upstream's count; gsr_get_binning refuses such a forward (0 binds
+ *     upstream's lists). */
 enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_COLUMN_PAIRS = 10,
-       GSR_OPT_COMPACT_SORT = 11 };
+       GSR_OPT_COMPACT_SORT = 11, GSR_OPT_TIGHT_BINNING = 12 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
 
 #ifdef __cplusplus

@@ -4,6 +4,9 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+import contextlib
+
+from gaussiansplattingviewer_amd import _lib
 from gaussiansplattingviewer_amd.camera import cuda_camera_inputs
 from gaussiansplattingviewer_amd.rasterizer import binning_state, rasterize_gaussians_native
 
@@ -25,6 +28,23 @@ def run_oracle(oracle, s, colors_precomp=None, cov3D_precomp=None):
                           scales=g.scale if use_sr else None, rotations=g.rot if use_sr else None,
                           scale_modifier=s["scale_modifier"], colors_precomp=colors_precomp,
                           cov3D_precomp=cov3D_precomp, bg=s["bg"])
+
+
+def set_option(dev, opt, value, slot=0):
+    lib = _lib.load_library()
+    _lib.check(lib.gsr_set_option(_lib.context(dev.index or 0, slot), opt, int(value)),
+               "gsr_set_option")
+
+
+@contextlib.contextmanager
+def tight_binning(dev, on, slot=0):
+    """GSR_OPT_TIGHT_BINNING for the block (default 1 restored after): 0 makes a forward
+    without n_contrib bin upstream's full 3-sigma lists, which gsr_get_binning exports."""
+    set_option(dev, _lib.GSR_OPT_TIGHT_BINNING, on, slot)
+    try:
+        yield
+    finally:
+        set_option(dev, _lib.GSR_OPT_TIGHT_BINNING, 1, slot)
 
 
 def to_dev(a, dev):

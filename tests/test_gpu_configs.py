@@ -23,7 +23,8 @@ from gaussiansplattingviewer_amd.pipeline import FramePipeline
 from gaussiansplattingviewer_amd.rasterizer import binning_state
 from gaussiansplattingviewer_amd.strips import strip_pixel_rows, strip_rows
 
-from gpu_helpers import ALL_EXTRAS, assert_parity, run_hip, run_oracle, scene_inputs, to_dev
+from gpu_helpers import (ALL_EXTRAS, assert_parity, run_hip, run_oracle, scene_inputs,
+                         tight_binning, to_dev)
 from gaussiansplattingviewer_amd.rasterizer import rasterize_gaussians_native
 
 pytestmark = pytest.mark.gpu
@@ -184,7 +185,8 @@ def test_c3r_balanced_strips_bit_identical(gpu, c3r, c3r_hip):
     full = c3r_hip
     W, H = s["W"], s["H"]
     gy, gx = (H + 15) // 16, (W + 15) // 16
-    run_hip(s, gpu, binning=False, extras=())  # the context's last forward: the full frame
+    with tight_binning(gpu, 0):  # the context's last forward: the full frame, upstream's lists
+        run_hip(s, gpu, binning=False, extras=())
     rp = tile_row_pairs(gy).cpu().numpy().view(np.uint32).astype(np.int64)
     rg = full["ranges"].astype(np.int64).reshape(gy, gx, 2)
     np.testing.assert_array_equal(rp, (rg[..., 1] - rg[..., 0]).sum(axis=1))

@@ -11,7 +11,8 @@ from gaussiansplattingviewer_amd.gaussian_data import synthetic_gaussians
 from gaussiansplattingviewer_amd.rasterizer import (GaussianRasterizationSettings,
                                                     GaussianRasterizer, binning_state)
 
-from gpu_helpers import assert_image_close, run_hip, run_oracle, scene_inputs, to_dev
+from gpu_helpers import (assert_image_close, run_hip, run_oracle, scene_inputs, tight_binning,
+                         to_dev)
 
 pytestmark = pytest.mark.gpu
 
@@ -30,15 +31,19 @@ def _args(s, dev):
 @pytest.mark.parametrize("P,W,H", [(20_000, 640, 480), (200_000, 1920, 1080)])
 def test_extension_matches_ctypes_entry_and_oracle(gpu, oracle_mod, P, W, H):
     s = scene_inputs(synthetic_gaussians(P, 3, seed=7), static_camera(W, H), 3)
-    num_rendered, color, radii, geom, binning, img = _C.rasterize_gaussians(*_args(s, gpu))
+    # the viewer's call (tight binning, the default), then upstream's full lists for the export
+    tight_color = _C.rasterize_gaussians(*_args(s, gpu))[1].cpu().numpy()
+    with tight_binning(gpu, 0):
+        num_rendered, color, radii, geom, binning, img = _C.rasterize_gaussians(*_args(s, gpu))
+        pl, _, rg = binning_state(gpu.index or 0)  # the shared slot-0 context's binning
     assert color.device == gpu and tuple(color.shape) == (3, H, W)
     assert radii.dtype == torch.int32 and tuple(radii.shape) == (P,)
     for b in (geom, binning, img):
         assert b.dtype == torch.uint8 and b.numel() == 0
-    pl, _, rg = binning_state(gpu.index or 0)  # the shared slot-0 context's binning
     pl = pl.cpu().numpy().view(np.uint32)
     rg = rg.cpu().numpy().view(np.uint32)
     color, radii = color.cpu().numpy(), radii.cpu().numpy()
+    np.testing.assert_array_equal(tight_color, color)  # the same splats in the same order
     ref = run_hip(s, gpu, extras=(), binning=False)
     assert num_rendered == ref["num_rendered"]
     np.testing.assert_array_equal(radii, ref["radii"])

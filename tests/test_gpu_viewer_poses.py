@@ -11,7 +11,9 @@ oracle then renders the same raster settings (the matrices the renderer uploaded
 sit at |position| ~ 0.8-2.6, i.e. inside the U(-2, 2)^3 cloud: real viewer orientations with
 Gaussians right in front of the camera, which exercise the z <= 0.2 cull, the 1.3 tan(fov)
 clamp of the EWA Jacobian and splats covering large parts of the window.  Bar: radii, K, the
-point list and the tile ranges bit-exact; the image within tests/gpu_helpers.py's tolerance.
+point list and the tile ranges bit-exact (with GSR_OPT_TIGHT_BINNING 0: upstream's lists); the
+image within tests/gpu_helpers.py's tolerance, and the default tight binning's image bit-identical
+to the full lists' one.
 """
 import os
 
@@ -24,7 +26,7 @@ from gaussiansplattingviewer_amd.gaussian_data import synthetic_gaussians
 from gaussiansplattingviewer_amd.rasterizer import binning_state
 from gaussiansplattingviewer_amd.renderer import HIPRenderer
 
-from gpu_helpers import assert_image_close
+from gpu_helpers import assert_image_close, tight_binning
 
 pytestmark = pytest.mark.gpu
 
@@ -53,9 +55,12 @@ def test_reference_viewer_pose(gpu, oracle_mod, viewer, i):
     cam = Camera(H, W)
     viewer.update_camera_intrin(cam)
     viewer.update_camera_pose(cam, True, POSES[i])
-    img = viewer.draw().cpu().numpy()
-    radii = viewer.radii.cpu().numpy()
-    pl, pt, rg = binning_state(gpu.index or 0)
+    tight_img = viewer.draw().cpu().numpy()
+    with tight_binning(gpu, 0):
+        img = viewer.draw().cpu().numpy()
+        radii = viewer.radii.cpu().numpy()
+        pl, pt, rg = binning_state(gpu.index or 0)
+    np.testing.assert_array_equal(tight_img, img)
 
     rs = viewer.raster_settings
     g = viewer.gaussians
