@@ -696,6 +696,10 @@ namespace {
 // over the K sorted keys on the main stream (the packed pair list has no tile keys to scan).
 constexpr int kDiffThreads = 1024;
 
+// kTight: the {rect, span word} records, column-major differences (two atomics per kept column,
+// then a prefix down each column); else the rects, row-major differences (two atomics per rect
+// row -- a strip clips the rows but not the columns -- then a prefix along each row).
+template <bool kTight>
 __global__ __launch_bounds__(kDiffThreads) void k_tile_diff(const uint2 *__restrict__ strip_rect,
                                                             const uint4 *__restrict__ strip_rc,
                                                             int64_t P, uint32_t gx, uint32_t rows,
@@ -714,7 +718,7 @@ __global__ __launch_bounds__(kDiffThreads) void k_tile_diff(const uint2 *__restr
         for (int k = 0; k < kU; ++k) {
             const int64_t j = i + (int64_t)k * kDiffThreads;
             r[k] = q[k] = make_uint2(0u, 0u);
-            if (j < b1 && strip_rc) {
+            if (j < b1 && kTight) {  // the rect and its span word, one load
                 const uint4 rq = strip_rc[j];
                 r[k] = make_uint2(rq.x, rq.y);
                 q[k] = make_uint2(rq.z, rq.w);
@@ -726,7 +730,14 @@ __global__ __launch_bounds__(kDiffThreads) void k_tile_diff(const uint2 *__restr
         for (int k = 0; k < kU; ++k) {
             if (r[k].x == 0u) continue;  // no pairs in the strip (a rect with pairs has width > 0)
             const uint32_t x0 = r[k].x & 0xFFFFu, w = r[k].x >> 16, y0 = r[k].y & 0xFFFFu;
-            const bool coded = strip_rc && span_coded(r[k]);
+            if (!kTight) {
+                for (uint32_t y = y0; y < y0 + (r[k].y >> 16); ++y) {
+                    atomicAdd(&s_diff[y * w1 + x0], 1u);
+                    atomicAdd(&s_diff[y * w1 + x0 + w], 0xFFFFFFFFu);  // -1 (mod 2^32)
+                }
+                continue;
+            }
+            const bool coded = span_coded(r[k]);
             // column x0 + c holds rows [y0 + lo, y0 + lo + cnt): +1 / -1 down the column
             for (uint32_t c = 0; c < w; ++c) {
                 uint32_t lo = 0u, cnt = r[k].y >> 16;
@@ -739,17 +750,31 @@ __global__ __launch_bounds__(kDiffThreads) void k_tile_diff(const uint2 *__restr
         }
     }
     __syncthreads();
-    // per column, the prefix down the rows: each tile's pair count (in place)
-    for (uint32_t x = threadIdx.x; x < gx; x += kDiffThreads) {
-        uint32_t run = 0u;
-        for (uint32_t y = 0; y < rows; ++y) {
-            run += s_diff[y * w1 + x];
-            s_diff[y * w1 + x] = run;
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    if (kTight) {
+        // per column, the prefix down the rows: each tile's pair count (in place)
+        for (uint32_t x = threadIdx.x; x < gx; x += kDiffThreads) {
+            uint32_t run = 0u;
+            for (uint32_t y = 0; y < rows; ++y) {
+                run += s_diff[y * w1 + x];
+                s_diff[y * w1 + x] = run;
+            }
+        }
+    } else {
+        // per row (a wave each), the prefix along the row
+        for (uint32_t y = wv; y < rows; y += kDiffThreads / 64) {
+            uint32_t carry = 0u;
+            for (uint32_t x0 = 0; x0 < gx; x0 += 64) {
+                const uint32_t x = x0 + ln;
+                const uint32_t v = x < gx ? s_diff[y * w1 + x] : 0u;
+                const uint32_t inc = wave_inclusive_scan(v) + carry;
+                if (x < gx) s_diff[y * w1 + x] = inc;
+                carry = __shfl(inc, 63);
+            }
         }
     }
     __syncthreads();
     // the rows' totals
-    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     for (uint32_t y = wv; y < rows; y += kDiffThreads / 64) {
         uint32_t acc = 0u;
         for (uint32_t x = ln; x < gx; x += 64) acc += s_diff[y * w1 + x];
@@ -821,16 +846,23 @@ hipError_t gsr_launch_tile_ranges_aux(const uint2 *strip_rect, const uint4 *stri
     if (e != hipSuccess) return e;
     const uint64_t bit = dev < 64 ? (1ull << dev) : 0ull;
     if (!bit || !(attr_done.load(std::memory_order_acquire) & bit)) {
-        e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_tile_diff),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kTileDiffMaxCells * 4);
-        if (e != hipSuccess) return e;
+        for (const void *fn : {reinterpret_cast<const void *>(&k_tile_diff<true>),
+                               reinterpret_cast<const void *>(&k_tile_diff<false>)}) {
+            e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    kTileDiffMaxCells * 4);
+            if (e != hipSuccess) return e;
+        }
         attr_done.fetch_or(bit, std::memory_order_release);
     }
     // one block per 16k rects (at least 64, at most kTileDiffBlocks): the rect pass stays
     // short at 6M Gaussians while the finalize's sum over the partials stays small at 1M
     const int nparts = (int)std::min<int64_t>(kTileDiffBlocks, std::max<int64_t>(64, (P + 16383) / 16384));
-    hipLaunchKernelGGL(k_tile_diff, dim3(nparts), dim3(kDiffThreads), lds, s, strip_rect,
-                       strip_rc, P, gx, rows, partial);
+    if (strip_rc)
+        hipLaunchKernelGGL(k_tile_diff<true>, dim3(nparts), dim3(kDiffThreads), lds, s, strip_rect,
+                           strip_rc, P, gx, rows, partial);
+    else
+        hipLaunchKernelGGL(k_tile_diff<false>, dim3(nparts), dim3(kDiffThreads), lds, s,
+                           strip_rect, strip_rc, P, gx, rows, partial);
     hipLaunchKernelGGL(k_tile_finalize, dim3(rows), dim3(kFinThreads), 0, s, partial,
                        nparts, gx, rows, ranges);
     return hipGetLastError();

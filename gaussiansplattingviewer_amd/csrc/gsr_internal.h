@@ -241,7 +241,7 @@ struct GsrPreprocessArgs {
     // {0, 0} when it has no pair in the strip (grid dimensions < 2^16, checked by the host)
     uint2 *strip_rect;
     // tight binning (else NULL): per Gaussian {strip rect, span word} (gsr::col_span; the span
-    // word is read only for span-coded rects), {0, 0, 0, 0} without pairs in the strip
+    // word only for span-coded rects), {0, 0, 0, 0} without pairs in the strip
     uint4 *strip_rc;
     // per k_preprocess block (ceil(P / 256)): its (Gaussian, strip tile) pair count (low 32
     // bits) and its pair count over the spans (high 32 bits: the same without tight binning),

@@ -195,52 +195,59 @@ __device__ __forceinline__ float3 cull_data(float A, float B, float C, float o) 
 // Span word of a span-coded strip rect (gsr_internal.h col_span): per column of the rect, the
 // tile rows whose pixel-centre box meets the ellipse q(d) = A dx^2 + 2B dx dy + C dy^2 <= 2 Lm
 // (cull_data's region, which holds every pixel where the blend can reach alpha >= 1/255),
-// widened outward.  Over a column's pixel-centre range dx in [ua, ub] the ellipse's dy extent is
-// reached at the column's edges or, if it lies inside, at the ellipse's top / bottom point.
-// Returns the pair count over the spans.  x0 / w: the rect's tile columns; sy0 / h: its
-// strip-clipped global tile rows.
+// widened outward.  A column's dx range is taken as [16 x - 0.5, 16 x + 15.5] - px, so
+// neighbouring columns share their boundary; over it the ellipse's dy extent is reached at the
+// boundaries or, if it lies inside, at the ellipse's top / bottom point.  Returns the pair count
+// over the spans.  x0 / w: the rect's tile columns; sy0 / h: its strip-clipped global tile rows.
 __device__ __forceinline__ uint32_t col_spans(float px, float py, float A, float B, float C,
                                               float Lm, uint32_t x0, uint32_t w, uint32_t sy0,
                                               uint32_t h, uint2 &cols) {
     uint64_t word = 0;
     for (uint32_t c = 0; c < w; ++c) word |= (uint64_t)(h << 4) << (8 * c);
     cols = make_uint2((uint32_t)word, (uint32_t)(word >> 32));
-    // the determinant in double (A C ~ B^2 for elongated splats), the rest in float with the
-    // hardware reciprocal / square root (1 ulp): their rounding (~1e-6 relative, ~1e-3 of vmax
-    // where the square root's argument cancels at the ellipse's u extremes) sits inside the
-    // margins (1e-5 on the threshold, 2e-3 vmax + 0.02 px on the extents)
-    const double det_d = (double)A * (double)C - (double)B * (double)B;
-    if (!(det_d > 0.0) || !(A > 0.0f) || !(C > 0.0f) || !(Lm < 1e30f) || !(fabsf(px) < 1e30f) ||
+    // the determinant with Kahan's compensated product (A C ~ B^2 for elongated splats), the
+    // rest in float with the hardware reciprocal / square root (1 ulp): their rounding (~1e-6
+    // relative, ~1e-3 of vmax where the square root's argument cancels at the ellipse's u
+    // extremes) sits inside the margins (1e-5 on the threshold, 2e-3 vmax + 0.02 px)
+    const float bb = B * B, det = __builtin_fmaf(A, C, -bb) - __builtin_fmaf(B, B, -bb);
+    if (!(det > 0.0f) || !(A > 0.0f) || !(C > 0.0f) || !(Lm < 1e30f) || !(fabsf(px) < 1e30f) ||
         !(fabsf(py) < 1e30f))
         return w * h;
-    const float det = (float)det_d, idet = __builtin_amdgcn_rcpf(det);
-    const float T2 = 2.0f * Lm * (1.0f + 1e-5f) + 1e-5f;
+    const float idet = __builtin_amdgcn_rcpf(det), T2 = 2.0f * Lm * (1.0f + 1e-5f) + 1e-5f;
     const float vmax = __builtin_amdgcn_sqrtf(A * T2 * idet);
     const float umax = __builtin_amdgcn_sqrtf(C * T2 * idet) * (1.0f + 1e-5f) + 0.02f;
-    if (!(vmax < 1e30f) || !(umax < 1e30f) || !(det > 0.0f)) return w * h;
+    if (!(vmax < 1e30f) || !(umax < 1e30f)) return w * h;
     const float ut = -B * vmax * __builtin_amdgcn_rcpf(A), ev = 2e-3f * vmax + 0.02f;
     const float rc = __builtin_amdgcn_rcpf(C), cT2 = C * T2;
     // rows relative to the rect: [lo, hi] clamped to [0, h - 1]
     const float ylo = py - ev - 15.0f - 16.0f * (float)sy0, yhi = py + ev - 16.0f * (float)sy0;
     const float hmax = (float)(h - 1);
+    // boundary k: dx = 16 (x0 + k) - 0.5 - px clamped to the ellipse, its dy extent [dn, up]
+    float b = 16.0f * (float)x0 - 0.5f - px;
+    float u0 = fminf(fmaxf(b, -umax), umax);
+    float h0 = __builtin_amdgcn_sqrtf(fmaxf(0.0f, cT2 - det * u0 * u0));
+    float up0 = (-B * u0 + h0) * rc, dn0 = (-B * u0 - h0) * rc;
     word = 0;
     uint32_t pairs = 0;
-#pragma unroll 1
-    for (uint32_t c = 0; c < w; ++c) {
-        const float cx = 16.0f * (float)(x0 + c);
-        const float ua = fmaxf(cx - px, -umax), ub = fminf(cx + 15.0f - px, umax);
-        if (!(ua <= ub)) continue;
-        const float ha = __builtin_amdgcn_sqrtf(fmaxf(0.0f, cT2 - det * ua * ua));
-        const float hb = __builtin_amdgcn_sqrtf(fmaxf(0.0f, cT2 - det * ub * ub));
-        const float vhi = (ut >= ua && ut <= ub) ? vmax : fmaxf(-B * ua + ha, -B * ub + hb) * rc;
-        const float vlo = (-ut >= ua && -ut <= ub) ? -vmax : fminf(-B * ua - ha, -B * ub - hb) * rc;
-        const float lo = fmaxf(ceilf((ylo + vlo) * 0.0625f), 0.0f);
-        const float hi = fminf(floorf((yhi + vhi) * 0.0625f), hmax);
-        if (lo <= hi) {
-            const uint32_t l = (uint32_t)lo, n = (uint32_t)(hi - lo) + 1u;
-            word |= (uint64_t)(l | (n << 4)) << (8 * c);
-            pairs += n;
+#pragma unroll
+    for (uint32_t c = 0; c < kSpanCols; ++c) {
+        if (c >= w) break;
+        const float b1 = b + 16.0f;
+        const float u1 = fminf(fmaxf(b1, -umax), umax);
+        const float h1 = __builtin_amdgcn_sqrtf(fmaxf(0.0f, cT2 - det * u1 * u1));
+        const float up1 = (-B * u1 + h1) * rc, dn1 = (-B * u1 - h1) * rc;
+        if (b <= umax && b1 >= -umax) {
+            const float vhi = (ut >= u0 && ut <= u1) ? vmax : fmaxf(up0, up1);
+            const float vlo = (-ut >= u0 && -ut <= u1) ? -vmax : fminf(dn0, dn1);
+            const float lo = fmaxf(ceilf((ylo + vlo) * 0.0625f), 0.0f);
+            const float hi = fminf(floorf((yhi + vhi) * 0.0625f), hmax);
+            if (lo <= hi) {
+                const uint32_t l = (uint32_t)lo, n = (uint32_t)(hi - lo) + 1u;
+                word |= (uint64_t)(l | (n << 4)) << (8 * c);
+                pairs += n;
+            }
         }
+        b = b1, u0 = u1, up0 = up1, dn0 = dn1;
     }
     cols = make_uint2((uint32_t)word, (uint32_t)(word >> 32));
     return pairs;
