@@ -369,7 +369,7 @@ int setup_frame(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     // frames only: on a strip the replicated preprocess writes a 16-B record for every Gaussian
     // to shorten one strip's lists (C4 3/8 strip: preprocess 97 -> 141 us, row pass 52 -> 42 us;
     // C3 3/8 strip 0.150 -> 0.157 ms per frame; DESIGN.md decision 11)
-    f.tight = ctx->tight && f.colpairs && !out->n_contrib;
+    f.tight = ctx->tight && f.colpairs && !out->n_contrib && f.rows_tiles == f.gy;
     pa.strip_rc = f.tight ? static_cast<uint4 *>(ctx->strip_rc.p) : nullptr;
     pa.block_pairs = static_cast<uint64_t *>(ctx->pair_count.p);
     pa.host_K = ctx->d_hostK;

@@ -710,24 +710,21 @@ __global__ __launch_bounds__(kDiffThreads) void k_tile_diff(const uint2 *__restr
     for (uint32_t c = threadIdx.x; c < cells; c += kDiffThreads) s_diff[c] = 0u;
     __syncthreads();
     const int64_t b0 = P * blockIdx.x / gridDim.x, b1 = P * (blockIdx.x + 1) / gridDim.x;
-    // 4 rects per thread and step, their loads issued together; with kTight the span words
-    // then only for the rects with pairs (strip_rc is not written for the others: on a strip
-    // most Gaussians have none)
+    // 4 rects per thread and step, their loads issued together
     constexpr int kU = 4;
-    const uint2 *span_words = reinterpret_cast<const uint2 *>(strip_rc);
     for (int64_t i = b0 + threadIdx.x; i < b1; i += kU * kDiffThreads) {
         uint2 r[kU], q[kU];
 #pragma unroll
         for (int k = 0; k < kU; ++k) {
             const int64_t j = i + (int64_t)k * kDiffThreads;
             r[k] = q[k] = make_uint2(0u, 0u);
-            if (j < b1) r[k] = strip_rect[j];
-        }
-        if (kTight) {
-#pragma unroll
-            for (int k = 0; k < kU; ++k)
-                if (r[k].x != 0u && span_coded(r[k]))
-                    q[k] = span_words[2 * (i + (int64_t)k * kDiffThreads) + 1];
+            if (j < b1 && kTight) {  // the rect and its span word, one load
+                const uint4 rq = strip_rc[j];
+                r[k] = make_uint2(rq.x, rq.y);
+                q[k] = make_uint2(rq.z, rq.w);
+            } else if (j < b1) {
+                r[k] = strip_rect[j];
+            }
         }
 #pragma unroll
         for (int k = 0; k < kU; ++k) {

@@ -327,7 +327,8 @@ __device__ __forceinline__ Front front_one(const GsrPreprocessArgs &a, int64_t i
 // The outputs of a Gaussian without a pair in the strip (strip_skip: radii and the
 // per-Gaussian extras are not requested).
 __device__ __forceinline__ void none_one(const GsrPreprocessArgs &a, int64_t idx) {
-    a.strip_rect[idx] = make_uint2(0u, 0u);  // (strip_rc is read only where this is nonzero)
+    a.strip_rect[idx] = make_uint2(0u, 0u);
+    if (a.strip_rc) a.strip_rc[idx] = make_uint4(0u, 0u, 0u, 0u);
     a.sort_keys[idx] = 0xFFFFFFFFu;
 }
 
@@ -395,9 +396,7 @@ __device__ __forceinline__ uint32_t back_one(const GsrPreprocessArgs &a, int64_t
     }
     if (a.radii) a.radii[idx] = radius_out;
     a.strip_rect[idx] = strip_rect;
-    // strip_rc only for a Gaussian with pairs in the strip: every reader tests the rect first
-    if (a.strip_rc && strip_rect.x)
-        a.strip_rc[idx] = make_uint4(strip_rect.x, strip_rect.y, cols.x, cols.y);
+    if (a.strip_rc) a.strip_rc[idx] = make_uint4(strip_rect.x, strip_rect.y, cols.x, cols.y);
     tight_out =
         (strip_rect.x && a.strip_rc && span_coded(strip_rect)) ? strip_tiles_tight : strip_tiles;
     a.sort_keys[idx] = key;  // the depth sort's values are the indices (implicit)

@@ -220,9 +220,9 @@ const char *gsr_stage_name(int i);
  *     Gaussian of a rect up to 8 tile columns x 15 rows is paired only with the tiles its
  *     alpha >= 1/255 ellipse reaches (upstream's blend skips it on the others), so the lists are
  *     subsequences of upstream's and every pixel composites the same splats in the same order.
- *     Full frames and strips (the span record is written only for a Gaussian with pairs in the
- *     strip).  num_rendered stays upstream's count; gsr_get_binning refuses such a forward (0
- *     binds upstream's lists). */
+ *     Full frames only (a strip's replicated preprocess would write a record per Gaussian for
+ *     one strip's lists).  num_rendered stays upstream's count; gsr_get_binning refuses such a
+ *     forward (0 binds upstream's lists). */
 enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_COLUMN_PAIRS = 10,
        GSR_OPT_COMPACT_SORT = 11, GSR_OPT_TIGHT_BINNING = 12 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
