@@ -13,13 +13,12 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # GSR_LIB: another build of the library (A/B builds in tools/ab.sh); default the in-tree libgsr.so
 LIB_PATH = os.environ.get("GSR_LIB") or os.path.join(_HERE, "libgsr.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 GSR_OPT_BLEND_CULL = 1
 GSR_OPT_BLEND_FAST = 2
-GSR_OPT_COLUMN_PAIRS = 10
 GSR_OPT_COMPACT_SORT = 11
-GSR_OPT_TIGHT_BINNING = 12
+GSR_OPT_TIGHT_BINNING = 13
 
 # Symbols include/gsr.h declares (checked by the CPU test suite).
 EXPORTED_SYMBOLS = (
@@ -144,7 +143,8 @@ def _native_shares_library() -> bool:
     """The `_native` extension links the in-tree libgsr.so; contexts are shared with it only
     when this module loaded that same file (not a GSR_LIB A/B build)."""
     default = os.path.join(_HERE, "libgsr.so")
-    return os.path.exists(LIB_PATH) and os.path.samefile(LIB_PATH, default)
+    return (os.path.exists(LIB_PATH) and os.path.exists(default) and
+            os.path.samefile(LIB_PATH, default))
 
 
 def context(device_index: int, slot: int = 0) -> ctypes.c_void_p:
@@ -154,7 +154,9 @@ def context(device_index: int, slot: int = 0) -> ctypes.c_void_p:
     second stream): frames rendered through different slots on different streams may be in
     flight at the same time (`pipeline.FramePipeline`).  Slot 0 is the context the `_C`
     extension (`_native.so`) renders with, so the upstream entry points and this module share
-    one workspace and `binning_state()` sees a `GaussianRasterizer` forward."""
+    one workspace and `binning_state()` sees a `GaussianRasterizer` forward (its tight lists
+    unless GSR_OPT_TIGHT_BINNING is 0).  Under GSR_LIB (an A/B build) slot 0 is a context of
+    that build, and `GaussianRasterizer` renders through it by ctypes instead of `_C`."""
     import torch
 
     lib = load_library()

@@ -18,7 +18,8 @@
 // per-pair form (offsets scan -> duplicate fused with the first tile-sort pass -> the remaining
 // passes -> tile ranges from the sorted keys) for the frames the column form cannot take: more
 // than 256 tile columns or strip rows, a difference array larger than LDS, or more Gaussians than
-// the packed pair word holds.  GSR_OPT_COLUMN_PAIRS = 0 forces the per-pair form (tests).
+// the packed pair word holds (the choice is automatic; tests reach the per-pair form with images
+// wider than 256 tiles).
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -112,7 +113,6 @@ struct gsr_context {
     // options (include/gsr.h)
     int cull = 1;
     int fast = 1;
-    int column_pairs = 1;
     int compact_sort = -1;
     int tight = 1;
     // stage timing: a ring of event sets, one per timed forward, read back after the timed region
@@ -313,7 +313,7 @@ int setup_frame(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     // the column pass ranks <= 256 columns and the packed word holds the strip row and the id
     const int ybits = f.rows_tiles > 1 ? bits_for(f.rows_tiles - 1) : 0;
     f.col_shift = 32 - ybits;
-    f.colpairs = ctx->column_pairs && f.gx <= 256 && f.rows_tiles <= 256 &&
+    f.colpairs = f.gx <= 256 && f.rows_tiles <= 256 &&
                  gsr_tile_diff_cells(f.gx, f.rows_tiles) <= kTileDiffMaxCells &&
                  (f.col_shift == 32 || (uint64_t)P <= (1ull << f.col_shift));
 
@@ -801,7 +801,6 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
             if (value < 0 || value > 1) return fail(GSR_E_INVALID, "gsr_set_option: fast 0..1");
             ctx->fast = (int)value;
             return GSR_OK;
-        case GSR_OPT_COLUMN_PAIRS: ctx->column_pairs = value ? 1 : 0; return GSR_OK;
         case GSR_OPT_TIGHT_BINNING: ctx->tight = value ? 1 : 0; return GSR_OK;
         case GSR_OPT_COMPACT_SORT:
             if (value < -1 || value > 1) return fail(GSR_E_INVALID, "gsr_set_option: compact -1..1");
@@ -860,10 +859,6 @@ int gsr_get_binning(gsr_context *ctx, uint32_t *point_list, uint32_t *point_tile
                     uint32_t *ranges, int64_t *num_rendered, int32_t *num_tiles, void *stream) {
     if (!ctx) return fail(GSR_E_INVALID, "gsr_get_binning: NULL context");
     if (!ctx->have_forward) return fail(GSR_E_STATE, "gsr_get_binning: no forward yet");
-    if (ctx->last_tight)
-        return fail(GSR_E_STATE, "gsr_get_binning: the last forward used tight binning (its lists "
-                                 "hold only the tiles each splat can reach); set "
-                                 "GSR_OPT_TIGHT_BINNING 0 or request n_contrib for upstream's lists");
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t K = ctx->last_list;
     const uint64_t T = (uint64_t)ctx->last_gx * ctx->last_gy;

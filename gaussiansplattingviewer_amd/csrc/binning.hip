@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kFW * 64) void k_dup_scatter(
                                   digit_total, keys_out, vals_out, sm, u.kv.keys, u.kv.vals);
 }
 
-// ---- column-first pair generation (the default binning; GSR_OPT_COLUMN_PAIRS) ------------------
+// ---- column-first pair generation (the default binning form, chosen per frame by api.hip) -----
 // The tile sort is LSD over (row, column): pass 1 by the column x, pass 2 by the row y.  Pass 1
 // needs no pair-level work: a Gaussian whose strip rect is [x0, x0+w) x [y0, y0+h) has h pairs
 // in each of its w columns, and in the stable column order those h pairs are contiguous (rows

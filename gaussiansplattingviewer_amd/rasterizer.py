@@ -196,7 +196,10 @@ class _RasterizeGaussians(torch.autograd.Function):
                 rs.scale_modifier, none(cov3Ds_precomp), rs.viewmatrix, rs.projmatrix,
                 rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, none(sh), rs.sh_degree,
                 rs.campos, rs.prefiltered, rs.debug)
-        num_rendered, color, radii, geom, binning, img = _C.rasterize_gaussians(*args)
+        if _lib._native_shares_library():
+            num_rendered, color, radii, geom, binning, img = _C.rasterize_gaussians(*args)
+        else:  # GSR_LIB (an A/B build): `_C` links the in-tree library, so render by ctypes
+            num_rendered, color, radii, _ = rasterize_gaussians_native(*args)
         ctx.num_rendered = num_rendered
         ctx.mark_non_differentiable(radii)
         return color, radii

@@ -39,7 +39,9 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 1
+/* 2 (round 4): option ids renumbered (GSR_OPT_COLUMN_PAIRS retired, tight binning moved to 13,
+ * ids 10 and 12 reserved), gsr_get_binning exports tight lists. */
+#define GSR_ABI_VERSION 2
 
 enum {
     GSR_OK = 0,
@@ -119,11 +121,15 @@ int gsr_reserve(gsr_context *ctx, int64_t P, int64_t K);
 int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings *s,
                 gsr_outputs *out, void *stream);
 
-/* Binning state of the last gsr_forward on this context.  Writes the sizes (K pairs, T tiles
- * of the whole frame) and, for each non-NULL caller-owned DEVICE buffer, copies:
- * point_list[K] Gaussian ids sorted by (tile, depth); point_tiles[K] their global tile ids;
- * ranges[2*T] = [start,end) per tile (tiles outside the strip stay 0,0, as upstream's memset
- * leaves unused tiles).  Call once with NULL buffers to size them.  Synchronises `stream`. */
+/* Binning state of the last gsr_forward on this context: the pair lists its blend read.  Writes
+ * the sizes (K list entries, T tiles of the whole frame) and, for each non-NULL caller-owned
+ * DEVICE buffer, copies: point_list[K] Gaussian ids sorted by (tile, depth); point_tiles[K]
+ * their global tile ids; ranges[2*T] = [start,end) per tile (tiles outside the strip stay 0,0,
+ * as upstream's memset leaves unused tiles).  With upstream's lists (GSR_OPT_TIGHT_BINNING 0, a
+ * strip, or a forward that asked for n_contrib) K is the forward's num_rendered; after a tight
+ * forward the lists are the tight ones and K <= num_rendered (each tile's list is an in-order
+ * subsequence of upstream's: tests/test_gpu_tight_pin.py checks that against the oracle).  Call
+ * once with NULL buffers to size them.  Synchronises `stream`. */
 int gsr_get_binning(gsr_context *ctx, uint32_t *point_list, uint32_t *point_tiles,
                     uint32_t *ranges, int64_t *num_rendered, int32_t *num_tiles, void *stream);
 
@@ -207,11 +213,6 @@ const char *gsr_stage_name(int i);
  *   GSR_OPT_BLEND_FAST (default 1): blend arithmetic with log2(e) folded into the conic, FMA
  *     contraction and the hardware exp2 (tolerance in tests/gpu_helpers.py); 0 keeps upstream's
  *     per-pixel operation order (IEEE, no FMA, ocml expf).
- *   GSR_OPT_COLUMN_PAIRS (default 1): column-first binning -- the first tile-sort pass runs on
- *     (Gaussian, tile column) segments of the depth-sorted Gaussians and the second sorts packed
- *     (tile row, Gaussian id) words, with the tile ranges from the rects on a second stream.
- *     Frames it cannot take (> 256 tile columns or strip rows, more Gaussians than the packed
- *     word holds) use the per-pair form; 0 forces the per-pair form.
  *   GSR_OPT_COMPACT_SORT (default -1 = auto): 1 = the depth sort first compacts the keys of the
  *     Gaussians with pairs in the strip and sorts only those; 0 = its first pass drops the others
  *     while it sorts; auto = compact on strips (a proper subset of the tile rows) of >= 4M
@@ -221,10 +222,14 @@ const char *gsr_stage_name(int i);
  *     alpha >= 1/255 ellipse reaches (upstream's blend skips it on the others), so the lists are
  *     subsequences of upstream's and every pixel composites the same splats in the same order.
  *     Full frames only (a strip's replicated preprocess would write a record per Gaussian for
- *     one strip's lists).  num_rendered stays upstream's count; gsr_get_binning refuses such a
- *     forward (0 binds upstream's lists). */
-enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_COLUMN_PAIRS = 10,
-       GSR_OPT_COMPACT_SORT = 11, GSR_OPT_TIGHT_BINNING = 12 };
+ *     one strip's lists).  num_rendered stays upstream's count; gsr_get_binning exports the
+ *     tight lists (0 binds upstream's lists).
+ * The binning form is chosen per frame: column-first (the first tile-sort pass on (Gaussian,
+ * tile column) segments, the second on packed (tile row, Gaussian id) words) up to 256 tile
+ * columns and strip rows, else the per-pair form; both produce the same lists.  Ids 10 and 12
+ * are retired (ABI 1's column-pairs and tight-binning options) and rejected. */
+enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_COMPACT_SORT = 11,
+       GSR_OPT_TIGHT_BINNING = 13 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
 
 #ifdef __cplusplus

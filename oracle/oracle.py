@@ -66,6 +66,11 @@ def lib() -> ctypes.CDLL:
         L.oracle_argsort_f32.argtypes = [vp, i64, vp]
         L.oracle_set_threads.restype = ctypes.c_int
         L.oracle_set_threads.argtypes = [ctypes.c_int]
+        L.oracle_check_tight.restype = i64
+        L.oracle_check_tight.argtypes = [ctypes.c_uint32, ctypes.c_uint32] + [vp] * 7
+        L.oracle_tight_model_check.restype = i64
+        L.oracle_tight_model_check.argtypes = [i64, vp, vp, vp, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_float, vp]
         _lib = L
     return _lib
 
@@ -86,9 +91,11 @@ def _p(a):
 
 def forward(means3D, opacities, viewmatrix, projmatrix, campos, tanfovx, tanfovy, W, H,
             shs=None, sh_degree=0, scales=None, rotations=None, scale_modifier=1.0,
-            colors_precomp=None, cov3D_precomp=None, bg=(0.0, 0.0, 0.0)) -> dict:
+            colors_precomp=None, cov3D_precomp=None, bg=(0.0, 0.0, 0.0),
+            stages="all") -> dict:
     """Full forward on the CPU.  Matrices are upstream's column-major layout (the row-major
-    bytes of view.T / (P @ view).T).  Returns every intermediate and output."""
+    bytes of view.T / (P @ view).T).  Returns every intermediate and output.  stages:
+    "preprocess" or "bin" stop after that stage (only its outputs are returned)."""
     L = lib()
     means3D = _c(means3D).reshape(-1, 3)
     P = len(means3D)
@@ -119,6 +126,10 @@ def forward(means3D, opacities, viewmatrix, projmatrix, campos, tanfovx, tanfovy
     cov3d = np.zeros((P, 6), np.float32)
     K = L.oracle_preprocess(ctypes.byref(inp), _p(depths), _p(radii), _p(means2D), _p(conic),
                             _p(rgb), _p(clamped), _p(tiles), _p(cov3d))
+    out = dict(num_rendered=int(K), depths=depths, radii=radii, means2D=means2D,
+               conic_opacity=conic, rgb=rgb, clamped=clamped, tiles_touched=tiles, cov3D=cov3d)
+    if stages == "preprocess":
+        return out
     gx, gy = (W + 15) // 16, (H + 15) // 16
     keys = np.zeros(max(K, 1), np.uint64)
     vals = np.zeros(max(K, 1), np.uint32)
@@ -128,6 +139,9 @@ def forward(means3D, opacities, viewmatrix, projmatrix, campos, tanfovx, tanfovy
     if rc != 0:
         raise RuntimeError(f"oracle_bin failed: {rc}")
     keys, vals = keys[:K], vals[:K]
+    out.update(point_keys=keys, point_list=vals, ranges=ranges)
+    if stages == "bin":
+        return out
     color = np.zeros((3, H, W), np.float32)
     final_T = np.zeros((H, W), np.float32)
     n_contrib = np.zeros((H, W), np.uint32)
@@ -135,10 +149,46 @@ def forward(means3D, opacities, viewmatrix, projmatrix, campos, tanfovx, tanfovy
     if P > 0:
         L.oracle_render(ctypes.byref(inp), _p(ranges), _p(vals), _p(means2D), _p(features),
                         _p(conic), _p(color), _p(final_T), _p(n_contrib))
-    return dict(num_rendered=int(K), depths=depths, radii=radii, means2D=means2D,
-                conic_opacity=conic, rgb=rgb, clamped=clamped, tiles_touched=tiles,
-                cov3D=cov3d, point_keys=keys, point_list=vals, ranges=ranges, color=color,
-                final_T=final_T, n_contrib=n_contrib)
+    out.update(color=color, final_T=final_T, n_contrib=n_contrib)
+    return out
+
+
+_TIGHT_KEYS = ("not_subsequence", "kept", "dropped", "dropped_reaching", "first_tile",
+               "first_id", "max_dropped_alpha_e9", "_")
+_MODEL_KEYS = ("span_coded", "rect_tiles", "dropped", "dropped_reaching", "first_id",
+               "max_dropped_alpha_e9", "too_large", "eight_columns")
+
+
+def check_tight(gx, gy, ranges_full, list_full, ranges_tight, list_tight, means2D,
+                conic_opacity) -> dict:
+    """Tight tile lists (the HIP path's GSR_OPT_TIGHT_BINNING) against the oracle's lists:
+    per tile, an in-order subsequence, and every dropped pair skipped (power > 0 or alpha <
+    1/255, the oracle's arithmetic) at all 256 pixel centres (tight_check.c)."""
+    rf = _c(ranges_full, np.uint32).reshape(-1)
+    rt = _c(ranges_tight, np.uint32).reshape(-1)
+    assert len(rf) == len(rt) == 2 * gx * gy
+    lf = _c(list_full, np.uint32).reshape(-1)
+    lt = _c(list_tight, np.uint32).reshape(-1)
+    m2 = _c(means2D).reshape(-1)
+    co = _c(conic_opacity).reshape(-1)
+    stats = np.zeros(8, np.int64)
+    lib().oracle_check_tight(int(gx), int(gy), _p(rf), _p(lf) if len(lf) else None, _p(rt),
+                             _p(lt) if len(lt) else None, _p(m2), _p(co), _p(stats))
+    return dict(zip(_TIGHT_KEYS, (int(v) for v in stats)))
+
+
+def tight_model_check(means2D, conic_opacity, radii, W, H, shrink=0.0) -> dict:
+    """The HIP tight-binning predicate restated in C (preprocess.hip cull_data + col_spans) on
+    the oracle's preprocess outputs: every tile it drops from a rect is checked at all 256
+    pixel centres (tight_check.c).  shrink > 0: the predicate without its rounding margins and
+    with its log-threshold scaled by (1 - shrink) -- a mutation the check must catch."""
+    m2 = _c(means2D).reshape(-1)
+    co = _c(conic_opacity).reshape(-1)
+    r = _c(radii, np.int32).reshape(-1)
+    stats = np.zeros(8, np.int64)
+    lib().oracle_tight_model_check(len(r), _p(m2), _p(co), _p(r), int(W), int(H), float(shrink),
+                                   _p(stats))
+    return dict(zip(_MODEL_KEYS, (int(v) for v in stats)))
 
 
 def view_depth(xyz, view) -> np.ndarray:

@@ -19,7 +19,7 @@ def scene_inputs(g, cam, sh_degree, bg=(0.0, 0.0, 0.0), scale_modifier=1.0):
                 sh_degree=sh_degree, bg=np.asarray(bg, np.float32), scale_modifier=scale_modifier)
 
 
-def run_oracle(oracle, s, colors_precomp=None, cov3D_precomp=None):
+def run_oracle(oracle, s, colors_precomp=None, cov3D_precomp=None, stages="all"):
     g = s["g"]
     use_sh = colors_precomp is None
     use_sr = cov3D_precomp is None
@@ -27,7 +27,7 @@ def run_oracle(oracle, s, colors_precomp=None, cov3D_precomp=None):
                           s["W"], s["H"], shs=g.sh if use_sh else None, sh_degree=s["sh_degree"],
                           scales=g.scale if use_sr else None, rotations=g.rot if use_sr else None,
                           scale_modifier=s["scale_modifier"], colors_precomp=colors_precomp,
-                          cov3D_precomp=cov3D_precomp, bg=s["bg"])
+                          cov3D_precomp=cov3D_precomp, bg=s["bg"], stages=stages)
 
 
 def set_option(dev, opt, value, slot=0):
@@ -96,8 +96,8 @@ def ulp_diff(a, b):
 # where the oracle rounds every product.  Both shift values by a few ulp and can flip the
 # alpha >= 1/255 or T < 1e-4 threshold of a rare pixel (one such flip moves it by <= alpha * rgb
 # ~ 1/255).  Bar: >= 99.99 % of values within 1e-5, every value within 4e-3, PSNR (peak 1)
-# >= 80 dB.  Measured on MI355X with the final round-3 build
-# (profiles/r03c_blend_error_vs_oracle.jsonl, both modes, C2, C3, c3r, C4 full frame, C5 frames
+# >= 80 dB.  Measured on MI355X with the final round-3 build, lib 726b24d0
+# (profiles/r03n_blend_error_vs_oracle.jsonl, both modes, C2, C3, c3r, C4 full frame, C5 frames
 # 0/250/500/750): max abs 2.3e-3 (C3, exact) / 1.8e-3 (C4, fast), at least 99.9992 % of values
 # within 1e-5 (c3r, fast), PSNR >= 118.6 dB, n_contrib mismatch <= 4.8e-6.
 IMG_ATOL = 1e-5

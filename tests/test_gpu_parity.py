@@ -283,7 +283,6 @@ def test_headline_config_c3(gpu, c3_oracle, fast):
 
 
 VARIANTS = {  # [(option, alternative value, default), ...]
-    "per_pair": [(_lib.GSR_OPT_COLUMN_PAIRS, 0, 1)],
     "no_cull": [(_lib.GSR_OPT_BLEND_CULL, 0, 1)],
     "compact_sort": [(_lib.GSR_OPT_COMPACT_SORT, 1, -1)],
 }
@@ -307,10 +306,10 @@ class _options:
 @pytest.mark.parametrize("variant", list(VARIANTS))
 @pytest.mark.parametrize("size", [(1920, 1080), (16, 16), (4200, 64)])
 def test_sort_implementations_agree(gpu, variant, size):
-    """The defaults (column-first binning, the blend's quadrant cull, the depth sort dropping
-    the off-strip keys in its first pass) and the alternatives -- the per-pair binning form, no
-    cull, a compacting depth sort -- give identical binning and images.  Sizes: 1 tile
-    (tbits = 0) and > 256 tile columns (the per-pair form either way)."""
+    """The defaults (the blend's quadrant cull, the depth sort dropping the off-strip keys in
+    its first pass) and the alternatives -- no cull, a compacting depth sort -- give identical
+    binning and images.  Sizes: 1 tile (tbits = 0), a column-first frame and > 256 tile columns
+    (the per-pair binning form, which api.hip picks for such frames)."""
     w, h = size
     P = 300_000 if w * h > 10_000 else 20_000
     s = scene_inputs(synthetic_gaussians(P, 3, 21), static_camera(w, h, (0.5, 0.2, 3.5)), 3)
@@ -326,11 +325,13 @@ def test_sort_implementations_agree(gpu, variant, size):
 def test_long_tile_lists_and_depth_ties(gpu, oracle_mod, variant):
     """Tiles covered by more than 2048 splats (multi-chunk digit runs in the tile sort, long
     blend lists) and half of the Gaussians at one depth (ties: upstream orders them by
-    Gaussian index, so the stable depth sort must keep index order)."""
+    Gaussian index, so the stable depth sort must keep index order).  per_pair: the same scene
+    in a 4128-px-wide frame (258 tile columns), which api.hip bins in the per-pair form."""
     g = synthetic_gaussians(15000, 3, 23)
     g.scale[:] = np.float32(0.3)
     g.xyz[:7000, 2] = np.float32(0.25)  # one depth for half of them
-    s = scene_inputs(g, static_camera(320, 240, (0, 0, 3.0)), 3)
+    w = 4128 if variant == "per_pair" else 320
+    s = scene_inputs(g, static_camera(w, 240, (0, 0, 3.0)), 3)
     orc = run_oracle(oracle_mod, s)
     counts = orc["ranges"][:, 1] - orc["ranges"][:, 0]
     assert counts.max() > 2048 and (counts > 2048).sum() > 10, counts.max()

@@ -94,7 +94,7 @@ def test_tight_in_every_blend_mode(gpu, scene, fast, cull):
     _same(tight, full)
 
 
-def test_tight_lists_are_shorter_and_export_is_refused(gpu):
+def test_tight_lists_are_shorter_and_exported(gpu):
     s = _scene("dense_720p")
     gy = (s["H"] + 15) // 16
     with tight_binning(gpu, 0):
@@ -104,12 +104,13 @@ def test_tight_lists_are_shorter_and_export_is_refused(gpu):
     rows = tile_row_pairs(gy).cpu().numpy().view(np.uint32).astype(np.int64)
     assert full_rows.sum() == res["num_rendered"]  # upstream's K either way
     assert np.all(rows <= full_rows) and rows.sum() < 0.8 * full_rows.sum(), (rows.sum(), full_rows.sum())
+    # gsr_get_binning exports the tight lists the blend read (their total, not upstream's K)
     lib = _lib.load_library()
     K = ctypes.c_int64()
     T = ctypes.c_int32()
     rc = lib.gsr_get_binning(_lib.context(gpu.index or 0), None, None, None, ctypes.byref(K),
                              ctypes.byref(T), None)
-    assert rc == -4 and b"tight" in lib.gsr_last_error()  # GSR_E_STATE
+    assert rc == 0 and K.value == rows.sum() and T.value == gy * ((s["W"] + 15) // 16)
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])

@@ -12,8 +12,10 @@ sit at |position| ~ 0.8-2.6, i.e. inside the U(-2, 2)^3 cloud: real viewer orien
 Gaussians right in front of the camera, which exercise the z <= 0.2 cull, the 1.3 tan(fov)
 clamp of the EWA Jacobian and splats covering large parts of the window.  Bar: radii, K, the
 point list and the tile ranges bit-exact (with GSR_OPT_TIGHT_BINNING 0: upstream's lists); the
-image within tests/gpu_helpers.py's tolerance, and the default tight binning's image bit-identical
-to the full lists' one.
+image within tests/gpu_helpers.py's tolerance; the default tight binning's image bit-identical
+to the full lists' one, and its exported lists pinned against the oracle's
+(test_gpu_tight_pin.pin_tight_lists: in-order subsequences, every dropped pair skipped at all
+256 pixel centres of its tile).
 """
 import os
 
@@ -27,6 +29,7 @@ from gaussiansplattingviewer_amd.rasterizer import binning_state
 from gaussiansplattingviewer_amd.renderer import HIPRenderer
 
 from gpu_helpers import assert_image_close, tight_binning
+from test_gpu_tight_pin import pin_tight_lists
 
 pytestmark = pytest.mark.gpu
 
@@ -56,6 +59,13 @@ def test_reference_viewer_pose(gpu, oracle_mod, viewer, i):
     viewer.update_camera_intrin(cam)
     viewer.update_camera_pose(cam, True, POSES[i])
     tight_img = viewer.draw().cpu().numpy()
+    shared = _lib._native_shares_library()  # not under a GSR_LIB A/B build: its own context
+    if shared:
+        tpl, tpt, trg = binning_state(gpu.index or 0)
+        tight = {"point_list": tpl.cpu().numpy().view(np.uint32),
+                 "point_tiles": tpt.cpu().numpy().view(np.uint32),
+                 "ranges": trg.cpu().numpy().view(np.uint32),
+                 "num_rendered": None, "radii": viewer.radii.cpu().numpy()}
     with tight_binning(gpu, 0):
         img = viewer.draw().cpu().numpy()
         radii = viewer.radii.cpu().numpy()
@@ -73,7 +83,8 @@ def test_reference_viewer_pose(gpu, oracle_mod, viewer, i):
     # every pose sees part of the scene except the last, saved 6.8 units out, looking away
     assert (orc["num_rendered"] > 0) == (i != 17)
     np.testing.assert_array_equal(radii, orc["radii"])
-    if _lib._native_shares_library():  # not under a GSR_LIB A/B build: its own context
+    if shared:
+        pin_tight_lists(oracle_mod, orc, tight, W, H)
         assert len(pl) == orc["num_rendered"]
         np.testing.assert_array_equal(pl.cpu().numpy().view(np.uint32), orc["point_list"])
         np.testing.assert_array_equal(pt.cpu().numpy().view(np.uint32),
