@@ -34,68 +34,95 @@ struct RsCount {
 };
 
 // Reduce-then-scan over tiles of kW waves x kIt keys per lane (8 x 8 = 4096 keys: the fastest
-// shape measured for the K-sized tile sort).  nb = hist column stride (tiles of the
-// host's upper bound).
-template <int kW, int kIt>
+// shape measured for the K-sized tile sort).  The histogram is digit-major,
+// hist[d * stride + tile] (the scan reads a digit's column contiguously), stride = the tile count
+// rounded up to a multiple of 4.  A block counts kTiles consecutive tiles and stores each
+// digit's kTiles counts as one word of 4 kTiles bytes: with one tile per block every 4-B store
+// lands on its own line (the 4K frame's upsweep wrote 278 MB for a 7 MB histogram), so large
+// passes take 4 tiles per block and write 16-B words (gsr_radix_hist_words pads the stride).
+template <int kW, int kIt, int kTiles>
 __global__ __launch_bounds__(kW * 64) void k_rs_upsweep(const uint32_t *__restrict__ keys,
                                                         int64_t n, int shift, uint32_t mask,
-                                                        uint32_t *__restrict__ hist, int64_t nb) {
+                                                        uint32_t *__restrict__ hist,
+                                                        int64_t stride) {
     constexpr int kThreads = kW * 64, kT = kThreads * kIt;
     static_assert(kIt % 4 == 0, "full tiles are read as uint4");
     static_assert(kW >= 4, "the digit scans take one thread per digit (256)");
+    static_assert(kTiles == 1 || kTiles == 4, "one tile or a 16-B word of four");
     __shared__ uint32_t s_hist[kW][kRadix];
     const int tid = threadIdx.x, w = tid >> 6;
-    const int64_t base = (int64_t)blockIdx.x * kT;
-    if (base >= n) return;  // whole block (the scan reads columns [0, ceil(n / kT)) only)
-    for (int i = tid; i < kW * kRadix; i += kThreads) (&s_hist[0][0])[i] = 0;
-    __syncthreads();
-    auto add = [&](uint32_t key) { atomicAdd(&s_hist[w][(key >> shift) & mask], 1u); };
-    if (base + kT <= n) {
-        const uint4 *k4 = reinterpret_cast<const uint4 *>(keys + base);
+    const int64_t tile0 = (int64_t)blockIdx.x * kTiles;
+    if (tile0 * kT >= n) return;  // whole block (the scan reads columns [0, ceil(n / kT)) only)
+    uint32_t cnt[kTiles];
+    for (int t = 0; t < kTiles; ++t) {
+        const int64_t base = (tile0 + t) * kT;
+        for (int i = tid; i < kW * kRadix; i += kThreads) (&s_hist[0][0])[i] = 0;
+        __syncthreads();
+        auto add = [&](uint32_t key) { atomicAdd(&s_hist[w][(key >> shift) & mask], 1u); };
+        if (base + kT <= n) {
+            const uint4 *k4 = reinterpret_cast<const uint4 *>(keys + base);
 #pragma unroll
-        for (int j = 0; j < kIt / 4; ++j) {
-            const uint4 q = k4[j * kThreads + tid];
-            add(q.x);
-            add(q.y);
-            add(q.z);
-            add(q.w);
+            for (int j = 0; j < kIt / 4; ++j) {
+                const uint4 q = k4[j * kThreads + tid];
+                add(q.x);
+                add(q.y);
+                add(q.z);
+                add(q.w);
+            }
+        } else {
+            for (int64_t e = base + tid; e < n; e += kThreads) add(keys[e]);
         }
-    } else {
-        for (int64_t e = base + tid; e < n; e += kThreads) add(keys[e]);
-    }
-    __syncthreads();
-    if (tid < kRadix) {
+        __syncthreads();
         uint32_t c = 0;
+        if (tid < kRadix) {
 #pragma unroll
-        for (int i = 0; i < kW; ++i) c += s_hist[i][tid];
-        hist[(int64_t)tid * nb + blockIdx.x] = c;
+            for (int i = 0; i < kW; ++i) c += s_hist[i][tid];
+        }
+        cnt[t] = c;
+        __syncthreads();  // s_hist is zeroed again for the next tile
+    }
+    if (tid < kRadix) {
+        if (kTiles == 4)
+            *reinterpret_cast<uint4 *>(hist + (int64_t)tid * stride + tile0) =
+                make_uint4(cnt[0], cnt[1 % kTiles], cnt[2 % kTiles], cnt[3 % kTiles]);
+        else
+            hist[(int64_t)tid * stride + tile0] = cnt[0];
     }
 }
 
-// One block per digit: exclusive scan of hist[d][0..ceil(n / kT)) (column stride nb) in
+// One block per digit: exclusive scan of hist[d][0..ceil(n / kT)) (column stride `stride`) in
 // place, total -> digit_total[d].
-__global__ __launch_bounds__(kBlock) void k_rs_scan(uint32_t *__restrict__ hist, int64_t nb,
+__global__ __launch_bounds__(kBlock) void k_rs_scan(uint32_t *__restrict__ hist, int64_t stride,
                                                     uint32_t *__restrict__ digit_total,
                                                     const RsCount cnt, int64_t kT) {
     __shared__ uint32_t s_tmp[4];
-    const int64_t nb_act = cnt.d_n ? ((int64_t)*cnt.d_n + kT - 1) / kT : nb;
-    uint32_t *h = hist + (int64_t)blockIdx.x * nb;
+    const int64_t nb_act = cnt.d_n ? ((int64_t)*cnt.d_n + kT - 1) / kT : cnt.n_host;
+    uint32_t *h = hist + (int64_t)blockIdx.x * stride;
     uint32_t carry = 0;
+    const bool vec = (stride & 3) == 0;  // 16-B aligned columns: whole words of 4 tiles
     for (int64_t start = 0; start < nb_act; start += kBlock * 4) {
         uint32_t v[4], sum = 0;
+        const int64_t e0 = start + threadIdx.x * 4;
+        if (vec && e0 + 3 < nb_act) {
+            const uint4 q = *reinterpret_cast<const uint4 *>(h + e0);
+            v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+        } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int64_t e = start + threadIdx.x * 4 + i;
-            v[i] = e < nb_act ? h[e] : 0u;
-            sum += v[i];
+            for (int i = 0; i < 4; ++i) v[i] = e0 + i < nb_act ? h[e0 + i] : 0u;
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sum += v[i];
         uint32_t total;
         uint32_t pre = block256_exclusive_scan(sum, s_tmp, total) + carry;
+        uint32_t o[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int64_t e = start + threadIdx.x * 4 + i;
-            if (e < nb_act) h[e] = pre;
-            pre += v[i];
+        for (int i = 0; i < 4; ++i) o[i] = pre, pre += v[i];
+        if (vec && e0 + 3 < nb_act) {
+            *reinterpret_cast<uint4 *>(h + e0) = make_uint4(o[0], o[1], o[2], o[3]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (e0 + i < nb_act) h[e0 + i] = o[i];
         }
         carry += total;
     }
@@ -151,7 +178,7 @@ GsrRadixPlan gsr_radix_plan(int begin_bit, int end_bit) {
 hipError_t gsr_launch_digit_scan(uint32_t *hist, int64_t nb, uint32_t *digit_total,
                                  hipStream_t s) {
     hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, nb, digit_total,
-                       RsCount{nb, nullptr}, (int64_t)1);
+                       RsCount{nb, nullptr}, (int64_t)1);  // (stride = column count here)
     return hipGetLastError();
 }
 
@@ -168,27 +195,38 @@ constexpr int kSW = 8, kSIt = 8;  // sort tile: 8 waves x 8 keys per lane
 constexpr int64_t kST = (int64_t)kSW * 64 * kSIt;
 }  // namespace
 
+// the histogram's column stride: tiles rounded up to a multiple of 4 (the 16-B upsweep words)
+static int64_t hist_stride(int64_t nb) { return (nb + 3) & ~(int64_t)3; }
+// passes of at least this many tiles count 4 tiles per upsweep block (16-B histogram words);
+// below it the grid would leave CUs idle (C3: 1,385 tiles)
+constexpr int64_t kQuadTiles = 4096;
+
 int64_t gsr_radix_hist_words(int64_t n) {
     const int64_t nb = (n + kST - 1) / kST;
-    return (nb < 1 ? 1 : nb) * kRadix;
+    return (nb < 1 ? 4 : hist_stride(nb)) * kRadix;
 }
 
 // One pass: upsweep, scan, downsweep.  v == nullptr: keys only.
 static void rts_pass(const uint32_t *k, const uint32_t *v, uint32_t *ko, uint32_t *vo, int64_t n,
                      int shift, int nbits, uint32_t *hist, uint32_t *digit_total, hipStream_t s) {
-    const int64_t nb = (n + kST - 1) / kST;  // grid and hist column stride
+    const int64_t nb = (n + kST - 1) / kST;  // tiles: the downsweep's grid
     if (nb == 0) return;
+    const int64_t stride = hist_stride(nb);
     const uint32_t mask = (1u << nbits) - 1u;
-    hipLaunchKernelGGL((k_rs_upsweep<kSW, kSIt>), dim3((unsigned)nb), dim3(kSW * 64), 0, s, k, n,
-                       shift, mask, hist, nb);
-    hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, nb, digit_total,
+    if (nb >= kQuadTiles)
+        hipLaunchKernelGGL((k_rs_upsweep<kSW, kSIt, 4>), dim3((unsigned)((nb + 3) / 4)),
+                           dim3(kSW * 64), 0, s, k, n, shift, mask, hist, stride);
+    else
+        hipLaunchKernelGGL((k_rs_upsweep<kSW, kSIt, 1>), dim3((unsigned)nb), dim3(kSW * 64), 0, s,
+                           k, n, shift, mask, hist, stride);
+    hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, stride, digit_total,
                        RsCount{nb, nullptr}, kST);
     if (v)
         hipLaunchKernelGGL((k_rs_downsweep<kSW, kSIt, true>), dim3((unsigned)nb), dim3(kSW * 64), 0,
-                           s, k, v, ko, vo, n, shift, nbits, hist, digit_total, nb);
+                           s, k, v, ko, vo, n, shift, nbits, hist, digit_total, stride);
     else
         hipLaunchKernelGGL((k_rs_downsweep<kSW, kSIt, false>), dim3((unsigned)nb), dim3(kSW * 64),
-                           0, s, k, v, ko, vo, n, shift, nbits, hist, digit_total, nb);
+                           0, s, k, v, ko, vo, n, shift, nbits, hist, digit_total, stride);
 }
 
 hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
