@@ -41,8 +41,7 @@ sys.path.insert(0, REPO)
 from gaussiansplattingviewer_amd import _lib  # noqa: E402
 from gaussiansplattingviewer_amd.camera import cuda_camera_inputs, orbit_eye, static_camera  # noqa: E402
 from gaussiansplattingviewer_amd.gaussian_data import clustered_scene, synthetic_gaussians  # noqa: E402
-from gaussiansplattingviewer_amd.rasterizer import (rasterize_gaussians_native, sh_planar,  # noqa: E402
-                                                    tile_row_pairs)
+from gaussiansplattingviewer_amd.rasterizer import rasterize_gaussians_native, tile_row_pairs  # noqa: E402
 from gaussiansplattingviewer_amd.pipeline import FramePipeline  # noqa: E402
 from gaussiansplattingviewer_amd.strips import (StripBalancer, StripGather, strip_pixel_rows,  # noqa: E402
                                                 strip_rows)
@@ -97,9 +96,6 @@ class Scene:
         up = lambda a: torch.as_tensor(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         self.xyz, self.rot, self.scale, self.opacity = up(g.xyz), up(g.rot), up(g.scale), up(g.opacity)
         self.sh = up(g.sh).reshape(P, -1, 3).contiguous()
-        # the renderer's coefficient-major SH copy, made once at upload as
-        # HIPRenderer.update_gaussian_data does (degree-3 storage only)
-        self.sh_planar = sh_planar(self.sh) if self.sh.shape[1] == 16 else None
         self.bg = torch.zeros(3, device=dev)
         self.dev = dev
         self.cams = []
@@ -118,7 +114,7 @@ class Scene:
                                           self.rot, 1.0, None, view, proj, tx, ty, self.H, self.W,
                                           self.sh, self.deg, campos, False, False,
                                           tile_rows=tile_rows, slot=slot, out_color=out_color,
-                                          radii=radii, sh_planar=self.sh_planar)
+                                          radii=radii)
 
 
 # Committed rocprofv3 profiles (tools/profile_config.sh on the GPU box, summarised here by

@@ -26,7 +26,7 @@ EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_get_binning", "gsr_mark_visible", "gsr_depth_argsort",
     "gsr_set_timing", "gsr_stage_times", "gsr_stage_name", "gsr_set_option",
     "gsr_ply_probe", "gsr_ply_load", "gsr_disparity_colors", "gsr_pack_image",
-    "gsr_tile_row_pairs", "gsr_sh_planar",
+    "gsr_tile_row_pairs",
 )
 
 GSR_PACK_RGBA_F32 = 0
@@ -41,7 +41,7 @@ class GsrGaussians(ctypes.Structure):
         ("means3D", ctypes.c_void_p), ("scales", ctypes.c_void_p),
         ("rotations", ctypes.c_void_p), ("opacities", ctypes.c_void_p),
         ("shs", ctypes.c_void_p), ("colors_precomp", ctypes.c_void_p),
-        ("cov3D_precomp", ctypes.c_void_p), ("shs_planar", ctypes.c_void_p),
+        ("cov3D_precomp", ctypes.c_void_p),
     ]
 
 
@@ -93,7 +93,6 @@ def _declare(lib: ctypes.CDLL) -> None:
                                     ctypes.POINTER(ctypes.c_int32), vp]
     lib.gsr_mark_visible.argtypes = [vp, vp, i64, vp, vp, vp, vp]
     lib.gsr_tile_row_pairs.argtypes = [vp, vp, i32, vp]
-    lib.gsr_sh_planar.argtypes = [vp, i64, i32, vp, vp]
     lib.gsr_depth_argsort.argtypes = [vp, vp, i64, ctypes.POINTER(ctypes.c_float), vp, vp, vp]
     lib.gsr_set_timing.argtypes = [vp, i32]
     lib.gsr_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_float), i32]
@@ -107,7 +106,7 @@ def _declare(lib: ctypes.CDLL) -> None:
                                          ctypes.POINTER(ctypes.c_float), ctypes.c_float, vp, vp]
     lib.gsr_pack_image.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                    ctypes.c_int32, vp, vp]
-    for name in ("gsr_sh_planar", "gsr_disparity_colors", "gsr_pack_image", "gsr_create", "gsr_reserve", "gsr_forward", "gsr_get_binning",
+    for name in ("gsr_disparity_colors", "gsr_pack_image", "gsr_create", "gsr_reserve", "gsr_forward", "gsr_get_binning",
                  "gsr_mark_visible", "gsr_depth_argsort", "gsr_set_timing", "gsr_tile_row_pairs",
                  "gsr_stage_times", "gsr_set_option", "gsr_ply_probe", "gsr_ply_load"):
         getattr(lib, name).restype = i32

@@ -337,10 +337,6 @@ int setup_frame(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     pa.rotations = g->rotations;
     pa.opacities = g->opacities;
     pa.shs = g->shs;
-    // the coefficient-major copy serves the degree-3 colour kernels (16-B aligned, M == 16)
-    pa.shs_planar = (g->shs_planar && g->shs && g->M == 16 &&
-                     (reinterpret_cast<uintptr_t>(g->shs_planar) & 15) == 0) ? g->shs_planar
-                                                                              : nullptr;
     pa.colors_precomp = g->colors_precomp;
     pa.cov3D_precomp = g->cov3D_precomp;
     pa.viewmatrix = st->viewmatrix;
@@ -910,15 +906,6 @@ int gsr_tile_row_pairs(gsr_context *ctx, uint32_t *row_pairs, int32_t n_rows, vo
     GSR_HIP(gsr_launch_row_pairs(static_cast<const uint2 *>(ctx->ranges_local.p), ctx->last_gx,
                                  rows, row_pairs, static_cast<hipStream_t>(stream)),
             "row pairs launch");
-    return GSR_OK;
-}
-
-int gsr_sh_planar(const float *shs, int64_t P, int32_t M, float *out, void *stream) {
-    if (P < 0 || M <= 0 || M > 16 || (P > 0 && (!shs || !out)) ||
-        (reinterpret_cast<uintptr_t>(out) & 15) != 0)
-        return fail(GSR_E_INVALID, "gsr_sh_planar: bad arguments (M in 1..16, out 16-B aligned)");
-    GSR_HIP(gsr_launch_sh_planar(shs, P, M, out, static_cast<hipStream_t>(stream)),
-            "sh planar launch");
     return GSR_OK;
 }
 

@@ -225,7 +225,6 @@ struct GsrPreprocessArgs {
     int D, M;
     float scale_modifier;
     const float *means3D, *scales, *rotations, *opacities, *shs, *colors_precomp, *cov3D_precomp;
-    const float *shs_planar;  // optional coefficient-major copy (gsr_gaussians.shs_planar)
     const float *viewmatrix, *projmatrix, *campos;
     float tanfovx, tanfovy, focal_x, focal_y;
     int W, H;
@@ -268,7 +267,6 @@ hipError_t gsr_launch_color_ids(const GsrPreprocessArgs &a, const uint32_t *ids,
 // K of the frame (sum of the preprocess blocks' pair counts), the pair count over the spans and
 // D -> a.host_K (pinned host memory), after the preprocess.
 hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s);
-hipError_t gsr_launch_sh_planar(const float *shs, int64_t P, int M, float *out, hipStream_t s);
 hipError_t gsr_launch_mark_visible(const float *means3D, int64_t P, const float *viewmatrix,
                                    uint8_t *visible, hipStream_t s);
 hipError_t gsr_launch_view_depth_keys(const float *xyz, int64_t P, float v20, float v21, float v22,

@@ -117,7 +117,7 @@ __device__ __forceinline__ float3 eval_sh(float3 pos, const float *campos, const
 // order, subtracted for basis 1 and 3 as upstream writes them -- but each coefficient is
 // consumed as it is read, so the row never sits in 48 registers.
 __device__ __forceinline__ float3 eval_sh3_stream(float3 pos, const float *campos,
-                                                  const float4 *row, int64_t stride) {
+                                                  const float4 *row) {
     float dx = pos.x - campos[0], dy = pos.y - campos[1], dz = pos.z - campos[2];
     const float len = sqrtf(dx * dx + dy * dy + dz * dz);
     dx = dx / len;
@@ -145,7 +145,7 @@ __device__ __forceinline__ float3 eval_sh3_stream(float3 pos, const float *campo
     float r[3];
 #pragma unroll
     for (int i = 0; i < 12; ++i) {
-        const float4 q = row[i * stride];
+        const float4 q = row[i];
         const float v[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -614,17 +614,6 @@ __device__ __forceinline__ void store_color(const GsrPreprocessArgs &a, int64_t 
     cc[3] = col.z;
 }
 
-// Gaussian idx's 12 float4 of degree-3 SH and their stride: the coefficient-major planes when
-// the caller gave them (a wave's loads of one plane are 1 KiB of consecutive bytes), else the
-// [P,16,3] row (12 consecutive float4; every lane on its own lines).
-__device__ __forceinline__ const float4 *sh_row(const GsrPreprocessArgs &a, int64_t idx) {
-    return a.shs_planar ? reinterpret_cast<const float4 *>(a.shs_planar) + idx
-                        : reinterpret_cast<const float4 *>(a.shs) + idx * 12;
-}
-__device__ __forceinline__ int64_t sh_stride(const GsrPreprocessArgs &a) {
-    return a.shs_planar ? a.P : 1;
-}
-
 // Degree 3 with 16-B aligned rows (the host launches k_color_generic otherwise), grid-stride
 // over waves of 64 Gaussians.  Every lane that needs a colour reads its own 192-B row with 12 x
 // 16-B loads and consumes the coefficients as they arrive (eval_sh3_stream, upstream's order).
@@ -648,7 +637,8 @@ __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
         if (idx < a.P && (a.rgb ? a.radii[idx] != 0 : a.strip_rect[idx].x != 0u)) {
             const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1],
                                          a.means3D[3 * idx + 2]);
-            store_color(a, idx, eval_sh3_stream(p, a.campos, sh_row(a, idx), sh_stride(a)));
+            store_color(a, idx, eval_sh3_stream(p, a.campos,
+                                                reinterpret_cast<const float4 *>(a.shs) + idx * 12));
         }
     }
     if (a.P < 0) s_occupancy_cap[threadIdx.x] = 0u;  // never: keeps the allocation referenced
@@ -667,28 +657,10 @@ __global__ __launch_bounds__(256) void k_color_ids(const GsrPreprocessArgs a,
         const int64_t idx = ids[i];
         const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1],
                                      a.means3D[3 * idx + 2]);
-        store_color(a, idx, eval_sh3_stream(p, a.campos, sh_row(a, idx), sh_stride(a)));
+        store_color(a, idx, eval_sh3_stream(p, a.campos,
+                                            reinterpret_cast<const float4 *>(a.shs) + idx * 12));
     }
     if (a.P < 0) s_occupancy_cap[threadIdx.x] = 0u;  // never: keeps the allocation referenced
-}
-
-// gsr_sh_planar: plane i of Gaussian p = floats [4i, 4i+4) of its 3M-float row (0 past 3M).
-// One thread per (p, plane); consecutive threads take consecutive p, so the stores are coalesced
-// and the row reads of a wave stay within 64 consecutive rows.
-__global__ __launch_bounds__(256) void k_sh_planar(const float *__restrict__ shs, int64_t P, int M,
-                                                   float4 *__restrict__ out) {
-    const int nvec = (3 * M + 3) / 4;
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= P * nvec) return;
-    const int i = (int)(t / P);
-    const int64_t p = t - (int64_t)i * P;
-    float v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int k = 4 * i + u;
-        v[u] = k < 3 * M ? shs[p * 3 * M + k] : 0.0f;
-    }
-    out[t] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
 // GaussianRasterizer.markVisible -> upstream markVisible kernel: in_frustum only.
@@ -732,7 +704,7 @@ hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, hipStream_t s) {
 hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int waves_per_simd, hipStream_t s) {
     if (a.P == 0) return hipSuccess;
     const unsigned g0 = grid_for(a.P);  // 4 waves of 64 Gaussians per block
-    if (!(a.sh_vec4 || a.shs_planar) || a.colors_precomp || a.D != 3) {
+    if (!a.sh_vec4 || a.colors_precomp || a.D != 3) {
         hipLaunchKernelGGL(k_color_generic, dim3(g0), dim3(256), 0, s, a);
         return hipGetLastError();
     }
@@ -753,7 +725,7 @@ hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int waves_per_simd, hipS
 }
 
 bool gsr_color_ids_ok(const GsrPreprocessArgs &a) {
-    return (a.sh_vec4 || a.shs_planar) && !a.colors_precomp && a.D == 3 && !a.rgb;
+    return a.sh_vec4 && !a.colors_precomp && a.D == 3 && !a.rgb;
 }
 
 hipError_t gsr_launch_color_ids(const GsrPreprocessArgs &a, const uint32_t *ids,
@@ -774,14 +746,6 @@ hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_publish_K, dim3(1), dim3(1024), 0, s,
                        reinterpret_cast<const unsigned long long *>(a.block_pairs), keybits,
                        (int64_t)g, a.host_K, a.k_tag);
-    return hipGetLastError();
-}
-
-hipError_t gsr_launch_sh_planar(const float *shs, int64_t P, int M, float *out, hipStream_t s) {
-    if (P == 0) return hipSuccess;
-    const int64_t n = P * ((3 * M + 3) / 4);
-    hipLaunchKernelGGL(k_sh_planar, dim3(grid_for(n)), dim3(256), 0, s, shs, P, M,
-                       reinterpret_cast<float4 *>(out));
     return hipGetLastError();
 }
 

@@ -69,7 +69,7 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
                                scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tanfovx,
                                tanfovy, image_height, image_width, sh, degree, campos, prefiltered,
                                debug, *, tile_rows=None, extras=(), stream=None, slot=0,
-                               out_color=None, radii=True, sh_planar=None) -> ForwardResult:
+                               out_color=None, radii=True) -> ForwardResult:
     """Same arguments, order and validation as upstream `_C.rasterize_gaussians`.
 
     Extensions (keyword-only, for the strip partition and the parity tests):
@@ -81,9 +81,7 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
       out_color -- preallocated contiguous f32 (3, rows, W) output (e.g. a gather buffer);
       radii     -- False (strips only, no per-Gaussian extras): no radii output
                    (ForwardResult.radii is None); Gaussians whose footprint bound misses the
-                   strip skip the per-Gaussian work (a multi-GPU strip rank needs its image only);
-      sh_planar -- the coefficient-major copy of `sh` (`sh_planar(sh)`, made once per scene):
-                   the degree-3 colour pass then reads coalesced planes (gsr.h shs_planar).
+                   strip skip the per-Gaussian work (a multi-GPU strip rank needs its image only).
     """
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
@@ -109,12 +107,6 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
     M = 0
     if sh is not None:
         M = int(sh.size(1)) if sh.ndimension() == 3 else int(sh.numel() // max(P, 1) // 3)
-    if sh_planar is not None:
-        want = ((3 * M + 3) // 4) * P * 4
-        if (sh is None or sh_planar.device != device or sh_planar.dtype != torch.float32 or
-                not sh_planar.is_contiguous() or sh_planar.numel() != want):
-            raise RuntimeError(f"sh_planar must be sh_planar(sh): a contiguous float32 tensor of "
-                               f"{want} values on {device}")
 
     gy = (H + 15) // 16
     if tile_rows is None:
@@ -160,8 +152,7 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
                           means3D=_lib.ptr(means3D), scales=_lib.ptr(scales),
                           rotations=_lib.ptr(rotations), opacities=_lib.ptr(opacities),
                           shs=_lib.ptr(sh), colors_precomp=_lib.ptr(colors_precomp),
-                          cov3D_precomp=_lib.ptr(cov3D_precomp),
-                          shs_planar=_lib.ptr(sh_planar) if sh is not None else None)
+                          cov3D_precomp=_lib.ptr(cov3D_precomp))
     st = _lib.GsrRasterSettings(image_width=W, image_height=H, tanfovx=float(tanfovx),
                                 tanfovy=float(tanfovy), viewmatrix=_lib.ptr(viewmatrix),
                                 projmatrix=_lib.ptr(projmatrix), campos=_lib.ptr(campos),
@@ -179,24 +170,6 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
         _lib.check(lib.gsr_forward(ctx, ctypes.byref(g), ctypes.byref(st), ctypes.byref(out),
                                    ctypes.c_void_p(stream)), "gsr_forward")
     return ForwardResult(int(out.num_rendered), color, radii, ext)
-
-
-def sh_planar(sh: torch.Tensor) -> torch.Tensor:
-    """The coefficient-major copy of (P, M, 3) SH rows (gsr_sh_planar): ceil(3M/4) planes of P
-    float4, as a flat float32 device tensor.  Made once per scene (HIPRenderer.update_gaussian_data);
-    rasterize_gaussians_native(..., sh_planar=) hands it to the colour pass."""
-    if not sh.is_cuda:
-        raise RuntimeError("sh_planar needs a device tensor")
-    sh = sh.float().contiguous()
-    P = int(sh.shape[0])
-    M = int(sh.numel() // max(P, 1) // 3)
-    out = torch.empty((((3 * M + 3) // 4) * max(P, 0) * 4,), dtype=torch.float32, device=sh.device)
-    lib = _lib.load_library()
-    with torch.cuda.device(sh.device):
-        _lib.check(lib.gsr_sh_planar(_lib.ptr(sh), P, M, _lib.ptr(out),
-                                     ctypes.c_void_p(torch.cuda.current_stream(sh.device).cuda_stream)),
-                   "gsr_sh_planar")
-    return out
 
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,

@@ -19,8 +19,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .rasterizer import (GaussianRasterizationSettings, GaussianRasterizer,
-                         rasterize_gaussians_native, sh_planar)
+from .rasterizer import GaussianRasterizationSettings, GaussianRasterizer, rasterize_gaussians_native
 
 
 class GaussianRenderBase:
@@ -56,14 +55,12 @@ class GaussianRenderBase:
 
 @dataclass
 class GaussianDataHIP:
-    """Device copy of the Gaussians (renderer_cuda.py:55-68 GaussianDataCUDA).  sh_planar: the
-    coefficient-major copy of sh the renderer adds at upload (rasterizer.sh_planar), or None."""
+    """Device copy of the Gaussians (renderer_cuda.py:55-68 GaussianDataCUDA)."""
     xyz: torch.Tensor
     rot: torch.Tensor
     scale: torch.Tensor
     opacity: torch.Tensor
     sh: torch.Tensor
-    sh_planar: torch.Tensor | None = None
 
     def __len__(self):
         return len(self.xyz)
@@ -87,9 +84,8 @@ def gaus_hip_from_cpu(gau, device="cuda") -> GaussianDataHIP:
 class HIPRenderer(GaussianRenderBase):
     """CUDARenderer's behaviour on the MI355X rasterizer (no GL)."""
 
-    def __init__(self, w, h, device="cuda", tile_rows=None, planar_sh=True):
+    def __init__(self, w, h, device="cuda", tile_rows=None):
         super().__init__()
-        self.planar_sh = planar_sh  # keep the coefficient-major SH copy (update_gaussian_data)
         self.device = torch.device(device)
         self.raster_settings = {
             "image_height": int(h),
@@ -115,14 +111,9 @@ class HIPRenderer(GaussianRenderBase):
 
     def update_gaussian_data(self, gaus):
         """renderer_cuda.py:135-137 (host GaussianData -> device); a GaussianDataHIP already on
-        the device (e.g. ply.load_ply(path, device=...)) is used as is.  For degree-3 storage the
-        renderer also keeps the coefficient-major copy of the SH rows (one kernel, once per
-        scene) that its colour pass reads coalesced (gsr.h shs_planar)."""
+        the device (e.g. ply.load_ply(path, device=...)) is used as is."""
         self.gaussians = gaus if isinstance(gaus, GaussianDataHIP) else gaus_hip_from_cpu(gaus, self.device)
         self.raster_settings["sh_degree"] = int(np.round(np.sqrt(self.gaussians.sh_dim))) - 1
-        g = self.gaussians
-        if self.planar_sh and g.sh_dim == 16 and g.sh_planar is None and len(g) > 0:
-            g.sh_planar = sh_planar(g.sh)
 
     def sort_and_update(self, camera, use_file=False, pose=None):
         pass  # the rasterizer sorts on the device every frame
@@ -194,19 +185,17 @@ class HIPRenderer(GaussianRenderBase):
         elif self.render_mod >= 0:
             settings["sh_degree"] = min(settings["sh_degree"], self.render_mod)
         rs = GaussianRasterizationSettings(**settings)
-        planar = g.sh_planar if shs is not None else None
         with torch.no_grad():
-            if self.tile_rows is None and planar is None:
-                # upstream's entry point, as renderer_cuda.py:211-224 calls it
+            if self.tile_rows is None:
                 img, radii = GaussianRasterizer(raster_settings=rs)(
                     means3D=g.xyz, means2D=None, shs=shs, colors_precomp=colors,
                     opacities=g.opacity, scales=g.scale, rotations=g.rot, cov3D_precomp=None)
-            else:  # the same forward, plus the strip or the coefficient-major SH copy
+            else:
                 res = rasterize_gaussians_native(
                     rs.bg, g.xyz, colors, g.opacity, g.scale, g.rot, rs.scale_modifier, None,
                     rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height,
                     rs.image_width, shs, rs.sh_degree, rs.campos, rs.prefiltered, rs.debug,
-                    tile_rows=self.tile_rows, sh_planar=planar)
+                    tile_rows=self.tile_rows)
                 img, radii = res.color, res.radii
         self.image, self.radii = img, radii
         return img

@@ -68,12 +68,6 @@ typedef struct {
     const float *shs;            /* [P,M,3] */
     const float *colors_precomp; /* [P,3]  */
     const float *cov3D_precomp;  /* [P,6]  upper triangle xx,xy,xz,yy,yz,zz */
-    /* optional (NULL = not given): the SH coefficients again, coefficient-major -- 12 planes of
-     * P float4, plane i holding floats [4i, 4i+4) of every Gaussian's 48-float row (written once
-     * at upload by gsr_sh_planar; M == 16 only).  A wave then reads its 64 Gaussians' float4 of
-     * one plane as 1 KiB of consecutive bytes, where the [P,16,3] rows put every lane on its own
-     * 192-B line; with `shs` unchanged alongside (upstream's layout, the other kernels). */
-    const float *shs_planar;
 } gsr_gaussians;
 
 /* GaussianRasterizationSettings (renderer_cuda.py:104-117). */
@@ -200,12 +194,6 @@ int gsr_disparity_colors(const float *means3D, int64_t P, const float *view_host
                          const float *proj_host16, float baseline, float *colors, void *stream);
 int gsr_pack_image(const float *chw, int32_t H, int32_t W, int32_t format, int32_t flip_rows,
                    void *out, void *stream);
-
-/* Coefficient-major copy of [P,M,3] SH rows for gsr_gaussians.shs_planar: out[(i*P + p)*4 + u]
- * = shs[p*3M + 4i + u] for plane i < ceil(3M/4) (0 past 3M).  Device pointers, on `stream`.
- * No reference counterpart: the layout the viewer uploads (renderer_cuda.py:87-98) stays the
- * input; HIPRenderer.update_gaussian_data adds this copy once per scene. */
-int gsr_sh_planar(const float *shs, int64_t P, int32_t M, float *out, void *stream);
 
 /* Stage timing (HIP events on the forward's stream, no extra synchronisation).
  * gsr_set_timing(1) starts recording one event set per forward (a ring of the last 256);

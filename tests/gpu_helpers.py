@@ -8,8 +8,7 @@ import contextlib
 
 from gaussiansplattingviewer_amd import _lib
 from gaussiansplattingviewer_amd.camera import cuda_camera_inputs
-from gaussiansplattingviewer_amd.rasterizer import (binning_state, rasterize_gaussians_native,
-                                                    sh_planar)
+from gaussiansplattingviewer_amd.rasterizer import binning_state, rasterize_gaussians_native
 
 ALL_EXTRAS = ("depths", "means2D", "conic_opacity", "rgb", "tiles_touched", "final_T", "n_contrib")
 
@@ -53,13 +52,10 @@ def to_dev(a, dev):
 
 
 def run_hip(s, dev, tile_rows=None, colors_precomp=None, cov3D_precomp=None, extras=ALL_EXTRAS,
-            binning=True, debug=False, radii=True, planar=False):
-    """planar: also hand the forward the coefficient-major SH copy (HIPRenderer's and the
-    bench's call; degree-3 storage)."""
+            binning=True, debug=False, radii=True):
     g = s["g"]
     P = len(g.xyz)
     sh = None if colors_precomp is not None else to_dev(g.sh.reshape(P, g.sh.shape[-1] // 3, 3), dev)
-    planar_sh = sh_planar(sh) if planar and sh is not None and sh.shape[1] == 16 else None
     use_sr = cov3D_precomp is None
     res = rasterize_gaussians_native(
         to_dev(s["bg"], dev), to_dev(g.xyz, dev), to_dev(colors_precomp, dev),
@@ -67,7 +63,7 @@ def run_hip(s, dev, tile_rows=None, colors_precomp=None, cov3D_precomp=None, ext
         to_dev(g.rot, dev) if use_sr else None, s["scale_modifier"], to_dev(cov3D_precomp, dev),
         to_dev(s["view"], dev), to_dev(s["proj"], dev), s["tx"], s["ty"], s["H"], s["W"], sh,
         s["sh_degree"], to_dev(s["campos"], dev), False, debug, tile_rows=tile_rows,
-        extras=extras, radii=radii, sh_planar=planar_sh)
+        extras=extras, radii=radii)
     out = {"num_rendered": res.num_rendered, "color": res.color.cpu().numpy(),
            "radii": None if res.radii is None else res.radii.cpu().numpy()}
     for k, v in res.extras.items():

@@ -65,26 +65,12 @@ def test_forward_parity(gpu, oracle_mod, name):
 
 
 def _assert_plain_call_identical(gpu, s, hip):
-    """The viewer's call (no extras: the blend's n_contrib-free variant and tight binning) renders
-    the same bits as the call with every extra output -- with upstream's SH rows and with the
-    coefficient-major SH copy HIPRenderer and the bench pass (degree-3 storage)."""
-    for planar in (False, True):
-        plain = run_hip(s, gpu, extras=(), binning=False, planar=planar)
-        np.testing.assert_array_equal(plain["color"].view(np.uint32), hip["color"].view(np.uint32))
-        np.testing.assert_array_equal(plain["radii"], hip["radii"])
-        assert plain["num_rendered"] == hip["num_rendered"]
-
-
-def test_planar_sh_rgb_bit_identical(gpu):
-    """The colour pass on the coefficient-major SH copy (gsr_sh_planar) computes the same rgb
-    bits as on upstream's [P,16,3] rows (same operations, same order), for every degree."""
-    s = scene_inputs(synthetic_gaussians(50_000, 3, 12), static_camera(800, 600), 3)
-    for deg in (0, 1, 2, 3):
-        s["sh_degree"] = deg
-        a = run_hip(s, gpu, binning=False)
-        b = run_hip(s, gpu, binning=False, planar=True)
-        for k in ("rgb", "color", "final_T", "n_contrib"):
-            np.testing.assert_array_equal(a[k].view(np.uint32), b[k].view(np.uint32), err_msg=k)
+    """The viewer's call (no extras: the blend's n_contrib-free, paired-slot variant) renders the
+    same bits as the call with every extra output."""
+    plain = run_hip(s, gpu, extras=(), binning=False)
+    np.testing.assert_array_equal(plain["color"].view(np.uint32), hip["color"].view(np.uint32))
+    np.testing.assert_array_equal(plain["radii"], hip["radii"])
+    assert plain["num_rendered"] == hip["num_rendered"]
 
 
 def test_naive_scene_viewer_window(gpu, oracle_mod):
@@ -408,9 +394,8 @@ def test_compacted_strip_colour_path(gpu):
                          ("n_contrib", full["n_contrib"][y0:y0 + n])):
                 np.testing.assert_array_equal(part[k].view(np.uint32), v.view(np.uint32), err_msg=k)
             np.testing.assert_array_equal(part["radii"], full["radii"])
-            for planar in (False, True):  # k_color_ids on the rows and on the planar SH copy
-                lean = run_hip(s, gpu, tile_rows=rows, extras=pix, radii=False, planar=planar)
-                for k in ("color", "final_T", "n_contrib", "point_list"):
-                    np.testing.assert_array_equal(lean[k], part[k], err_msg=k)
+            lean = run_hip(s, gpu, tile_rows=rows, extras=pix, radii=False)
+            for k in ("color", "final_T", "n_contrib", "point_list"):
+                np.testing.assert_array_equal(lean[k], part[k], err_msg=k)
     finally:
         _set_option(gpu, _lib.GSR_OPT_COMPACT_SORT, -1)

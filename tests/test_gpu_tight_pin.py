@@ -45,7 +45,7 @@ def pin_tight_lists(oracle_mod, orc, hip, W, H):
 
 def _run(gpu, oracle_mod, s):
     orc = run_oracle(oracle_mod, s, stages="bin")
-    hip = run_hip(s, gpu, extras=(), planar=True)  # the viewer's and the bench's call
+    hip = run_hip(s, gpu, extras=())
     return pin_tight_lists(oracle_mod, orc, hip, s["W"], s["H"])
 
 
