@@ -184,7 +184,9 @@ def blend_roofline(config, launch_ms, launch_ms_inflight, alg_bytes):
     (FETCH_SIZE x2 + WRITE_SIZE per launch over the live launch time) and, as a labelled
     diagnostic, SURVEY.md's algorithmic bytes 40 K + 12 W H over the launch time -- omitted when
     above 1, which shows the blend does not read every pair's record (a pixel stops once T <
-    1e-4, a quadrant once its 64 pixels have)."""
+    1e-4, a quadrant once its 64 pixels have).  frac uses the serial launch time (the kernel on
+    an otherwise idle chip); frac_inflight the blend's event time with frames in flight (the
+    timed frames' regime, where the next frame's kernels share the CUs)."""
     out = {"bound": "valu", "kernel": "blend", "achieved": None, "peak": round(VALU_PEAK_T, 2),
            "unit": "T lane-instr/s", "frac": None, "traffic": None,
            "launch_ms": round(launch_ms, 5),
@@ -199,7 +201,9 @@ def blend_roofline(config, launch_ms, launch_ms_inflight, alg_bytes):
         c, src = sq
         ach = c["SQ_INSTS_VALU"] * 64 / (launch_ms * 1e-3) / 1e12
         cyc = c["GRBM_GUI_ACTIVE"] / 8  # summed over the 8 XCDs
+        ach_if = c["SQ_INSTS_VALU"] * 64 / (launch_ms_inflight * 1e-3) / 1e12
         out.update(achieved=round(ach, 3), frac=round(ach / VALU_PEAK_T, 4),
+                   achieved_inflight=round(ach_if, 3), frac_inflight=round(ach_if / VALU_PEAK_T, 4),
                    valu_wave_instr_per_launch=int(c["SQ_INSTS_VALU"]),
                    waves_per_launch=int(c["SQ_WAVES"]),
                    valu_busy=round(c["SQ_INSTS_VALU"] * 2 / 1024 / cyc, 4), sq_source=src)
