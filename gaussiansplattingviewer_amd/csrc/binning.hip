@@ -336,8 +336,11 @@ __global__ __launch_bounds__(kFW * 64) void k_dup_scatter(
 // the fused duplicate; the pair list is identical (each tile's pairs in depth order, then
 // Gaussian index; tiles row-major).
 constexpr int kCG = 256;                // depth-sorted Gaussians per block, one per thread
-constexpr int kCW = 4, kCIt = 8;        // segment ranking: 4 waves x up to 8 items
-constexpr int kCSeg = kCW * 64 * kCIt;  // up to 2048 segments ranked per round
+// 4 waves x up to 4 items: rounds of 1024 segments (C3 blocks average ~900; larger blocks take
+// more rounds), so a block's LDS is ~20 KB and twice as many blocks share a CU as with rounds
+// of 2048 (C3 column scatter 42.7 -> 34.0 us with the owner-written segment map below)
+constexpr int kCW = 4, kCIt = 4;
+constexpr int kCSeg = kCW * 64 * kCIt;  // up to 1024 segments ranked per round
 static_assert(kCG == kRadixBins, "one thread per column in the column scans");
 
 struct ColScatterSmem {
@@ -346,6 +349,7 @@ struct ColScatterSmem {
     uint32_t colbase[kRadixBins], colw0[kRadixBins];
     uint32_t keys[kCSeg], vals[kCSeg];  // the round's segments by column
     uint32_t wpre[kCSeg + 1];           // pair offset of each sorted segment
+    uint8_t seg_g[kCSeg];               // the round's segment -> block Gaussian (owner-written)
     uint32_t tmp[4];
 };
 
@@ -371,6 +375,13 @@ __device__ __forceinline__ void col_round(uint32_t R, uint32_t rn, int pack_shif
                                           uint32_t *__restrict__ out, ColScatterSmem &c, Smem &sm) {
     constexpr int kSeg = kCW * 64 * kIt;
     const int tid = threadIdx.x;
+    // the round's segment -> Gaussian map, written by each Gaussian's own thread
+    {
+        const uint32_t s0 = c.seg0[tid], w = c.x0w[tid] >> 16;
+        const uint32_t cb = R > s0 ? R - s0 : 0u, ce = min(w, R + rn > s0 ? R + rn - s0 : 0u);
+        for (uint32_t cc = cb; cc < ce; ++cc) c.seg_g[s0 + cc - R] = (uint8_t)tid;
+    }
+    __syncthreads();
     uint32_t k[kIt], v[kIt];
 #pragma unroll
     for (int j = 0; j < kIt; ++j) {
@@ -379,12 +390,7 @@ __device__ __forceinline__ void col_round(uint32_t R, uint32_t rn, int pack_shif
         v[j] = 0u;
         if (slot < rn) {
             const uint32_t sg = R + slot;
-            int lo = 0, hi = kCG - 1;  // last Gaussian whose first segment is <= sg
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (c.seg0[mid] <= sg) lo = mid;
-                else hi = mid - 1;
-            }
+            const int lo = c.seg_g[slot];  // the Gaussian whose segments hold sg
             const uint32_t col = (c.x0w[lo] & 0xFFFFu) + (sg - c.seg0[lo]);
             uint32_t slo, sn;
             seg_span(c, (uint32_t)lo, col, slo, sn);
