@@ -17,7 +17,7 @@ ABI_VERSION = 2
 
 GSR_OPT_BLEND_CULL = 1
 GSR_OPT_BLEND_FAST = 2
-GSR_OPT_COMPACT_SORT = 11
+GSR_OPT_DEPTH_SORT = 11
 GSR_OPT_TIGHT_BINNING = 13
 
 # Symbols include/gsr.h declares (checked by the CPU test suite).

@@ -69,8 +69,11 @@ constexpr auto kSpinLimit = std::chrono::milliseconds(50);
 // by the host's submission rate, which the wait would hold to the GPU (DESIGN.md §3 decision 2).
 constexpr int64_t kWaitDPairs = 4 << 20;
 // The depth sort compacts the kept keys first on strips of at least this many Gaussians
-// (GSR_OPT_COMPACT_SORT auto): a 1/8 strip of C4 keeps ~1/8 of them (DESIGN.md decision 2).
+// (GSR_OPT_DEPTH_SORT auto): a 1/8 strip of C4 keeps ~1/8 of them (DESIGN.md decision 2).
 constexpr int64_t kCompactP = 4 << 20;
+// The MSD depth sort for frames whose previous frame's kept depth keys differed in <= this many
+// bits (setup_frame).
+constexpr uint32_t kMsdMaxD = 24;
 
 const char *kStageNames[kAllStages] = {"preprocess", "depth_sort", "scan",  "duplicate",
                                        "tile_sort",  "ranges",     "blend", "color"};
@@ -101,6 +104,7 @@ struct gsr_context {
     unsigned long long *d_hostK = nullptr;  // device view of h_total + 2
     unsigned long long *d_hostD = nullptr;  // device view of h_total + 4
     uint32_t sort_tag = 0;                  // frames rendered on this context (the pinned tags)
+    uint32_t last_D = 0;                    // key bits of the last frame's kept depths
     // state of the last forward (gsr_get_binning, gsr_tile_row_pairs)
     bool have_forward = false;
     int64_t last_K = 0;        // upstream's num_rendered
@@ -113,7 +117,7 @@ struct gsr_context {
     // options (include/gsr.h)
     int cull = 1;
     int fast = 1;
-    int compact_sort = -1;
+    int depth_sort = -1;  // GSR_OPT_DEPTH_SORT
     int tight = 1;
     // stage timing: a ring of event sets, one per timed forward, read back after the timed region
     int timing = 0;        // 0 off, 1 every stage, 2 the blend only, on every 8th forward
@@ -224,6 +228,7 @@ struct Frame {
     int tmode;  // this forward's timing: 0 none, 1 every stage, 2 the blend
     hipEvent_t *ev, *evc;
     bool compact_sort;  // the depth sort compacts the kept keys first
+    bool msd_sort;      // the depth sort's MSD pass + per-bucket local sort (else LSD passes)
     bool color_ids;     // the colour pass walks the compacted ids
     bool colpairs;      // column-first binning (else the per-pair form)
     int col_shift;      // column pairs: packed word = strip row << col_shift | Gaussian id
@@ -360,9 +365,16 @@ int setup_frame(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     pa.strip_skip = out->radii == nullptr ? 1 : 0;
     pa.records = static_cast<gsr::SplatRecord *>(ctx->records.p);
     pa.sort_keys = static_cast<uint32_t *>(ctx->sort_keys.p);
-    f.compact_sort = ctx->compact_sort < 0 ? (f.rows_tiles < f.gy && P >= kCompactP)
-                                           : ctx->compact_sort != 0;
+    f.compact_sort = ctx->depth_sort < 0 ? (f.rows_tiles < f.gy && P >= kCompactP)
+                                         : ctx->depth_sort == 1;
     pa.block_kept = f.compact_sort ? static_cast<uint32_t *>(ctx->block_kept.p) : nullptr;
+    // the MSD sort wants buckets of a few thousand keys: its 4096 buckets split the top 12 of the
+    // D varying key bits, which balances them when D <= 24 (depths within one or two float
+    // exponents, C2-C5).  Wider spreads (the clustered c3r, D = 31) crowd some buckets past the
+    // LDS sort, so they keep the LSD passes; the choice follows the previous frame's D (the
+    // result is the same either way, only the time differs)
+    f.msd_sort = ctx->depth_sort < 0 ? !f.compact_sort && ctx->last_D <= (uint32_t)kMsdMaxD
+                                     : ctx->depth_sort == 2;
     pa.strip_rect = static_cast<uint2 *>(ctx->strip_rect.p);
     // tight binning: the column-first form, and no n_contrib (upstream's n_contrib counts list
     // positions of the full 3-sigma pairs); span words only then (NULL: every rect full).  Full
@@ -406,6 +418,13 @@ int launch_depth_sort(gsr_context *ctx, const Frame &f, int p0, int p1) {
                                      f.color_ids ? static_cast<uint32_t *>(ctx->color_ids.p)
                                                  : nullptr,
                                      f.color_ids ? ctx->compacted : nullptr);
+    } else if (f.msd_sort) {
+        // MSD pass + per-bucket local sort, the whole sort at once (D from the preprocess blocks)
+        if (p0 != 0) return GSR_OK;  // (no later passes)
+        const int64_t nb = (f.P + 255) / 256;
+        e = gsr_depth_sort_msd(f.pa.sort_keys, f.P,
+                               reinterpret_cast<const uint2 *>(f.pa.block_pairs + nb), nb, ds_a,
+                               ds_b, perm, hist, digit_total, ctl, f.s, ctx->d_hostD, f.tag);
     } else {
         e = gsr_depth_sort(f.pa.sort_keys, f.P, 1, ds_a, ds_b, perm, hist, digit_total, ctl, p0,
                            p1, f.s, ctx->d_hostD, f.tag);
@@ -436,9 +455,11 @@ int launch_second_stream(gsr_context *ctx, const Frame &f) {
                                        static_cast<uint32_t *>(ctx->blend_order.p), as),
                 "blend order launch");
     }
-    // colour waves per SIMD (gsr_launch_color): 3 below 4M Gaussians, else 4 (sweeps on MI355X,
-    // C3 and a C4 strip, DESIGN.md decision 7)
-    const int color_waves = f.P < (4 << 20) ? 3 : 4;
+    // colour waves per SIMD (gsr_launch_color): 2 on a full frame, so the colour leaves the CUs
+    // to the binning chain it overlaps (C3 two frames in flight 3,890-3,918 -> 3,947-3,954
+    // frames/s, serial 0.317 -> 0.308 ms; C4 serial 2.09 -> 2.06 ms); 3 on a compacted strip
+    // (C4 1/8 strip 0.481 -> 0.468 ms).  profiles/r04n_ab_color_waves.txt, DESIGN.md decision 7
+    const int color_waves = f.color_ids ? 3 : 2;
     if (f.color_ids) {
         GSR_HIP(hipStreamWaitEvent(as, ctx->compacted, 0), "hipStreamWaitEvent(compacted)");
         GSR_HIP(gsr_launch_color_ids(f.pa, static_cast<const uint32_t *>(ctx->color_ids.p),
@@ -488,6 +509,7 @@ int wait_K(gsr_context *ctx, Frame &f) {
     if (!spin_on(&ctx->h_total[7], [&](uint64_t v) { return v == f.tag; }, tagv))
         GSR_HIP(hipStreamSynchronize(ctx->aux), "hipStreamSynchronize(pair count)");
     f.K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
+    ctx->last_D = (uint32_t)__atomic_load_n(&ctx->h_total[3], __ATOMIC_ACQUIRE);
     f.KL = f.tight ? __atomic_load_n(&ctx->h_total[5], __ATOMIC_ACQUIRE) : f.K;
     if (f.dbg) {
         uint32_t ctl2[2];
@@ -661,12 +683,15 @@ int forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings 
     // D (the bits in which the kept depth keys differ) arrives in pinned memory from pass 0's
     // scan, tagged with this frame, while pass 0's downsweep runs: the host then queues only the
     // passes D needs.  Without it every pass is queued and the unneeded ones exit at once.
-    int depth_passes = gsr_depth_sort_passes(32);  // all
-    uint64_t dv = 0;
-    if (ctx->last_K >= kWaitDPairs &&
-        spin_on(&ctx->h_total[4], [&](uint64_t v) { return (uint32_t)(v >> 32) == f.tag; }, dv))
-        depth_passes = gsr_depth_sort_passes((uint32_t)dv);
-    GSR_TRY(launch_depth_sort(ctx, f, 1, depth_passes));
+    if (!f.msd_sort) {  // the LSD sort: the passes D needs
+        int depth_passes = gsr_depth_sort_passes(32);  // all
+        uint64_t dv = 0;
+        if (ctx->last_K >= kWaitDPairs &&
+            spin_on(&ctx->h_total[4], [&](uint64_t v) { return (uint32_t)(v >> 32) == f.tag; },
+                    dv))
+            depth_passes = gsr_depth_sort_passes((uint32_t)dv);
+        GSR_TRY(launch_depth_sort(ctx, f, 1, depth_passes));
+    }
     GSR_TRY(stage_end(ctx, f, 1));
 
     // ---- 3. scan
@@ -802,9 +827,10 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
             ctx->fast = (int)value;
             return GSR_OK;
         case GSR_OPT_TIGHT_BINNING: ctx->tight = value ? 1 : 0; return GSR_OK;
-        case GSR_OPT_COMPACT_SORT:
-            if (value < -1 || value > 1) return fail(GSR_E_INVALID, "gsr_set_option: compact -1..1");
-            ctx->compact_sort = (int)value;
+        case GSR_OPT_DEPTH_SORT:
+            if (value < -1 || value > 2)
+                return fail(GSR_E_INVALID, "gsr_set_option: depth sort -1..2");
+            ctx->depth_sort = (int)value;
             return GSR_OK;
         default:
             return fail(GSR_E_INVALID, "gsr_set_option: unknown option " + std::to_string(option));

@@ -52,14 +52,18 @@ constexpr int kCtlHead = 4;
 __device__ __forceinline__ int pass_bits(int shift) { return min(kDBits, 32 - shift); }
 
 // kFirst: `in` is the n keys (uint32); else the previous pass's (key, id) pairs (uint2).
+// msd (first pass only): the pass sorts the top 12 of the D varying key bits, shift ctl[2]
+// (k_ds_bits), and k_ds_local finishes every bucket (gsr_depth_sort_msd).
 template <bool kFirst>
 __global__ __launch_bounds__(kDThreads) void k_ds_upsweep(const void *__restrict__ in,
                                                           int64_t n_host, int drop,
                                                           uint32_t *__restrict__ ctl, int shift,
                                                           uint32_t *__restrict__ hist,
-                                                          const uint32_t *__restrict__ d_n) {
+                                                          const uint32_t *__restrict__ d_n,
+                                                          int msd) {
     __shared__ uint32_t s_h[kDBins];
     __shared__ uint32_t s_red[3][kDW];
+    if (kFirst && msd) shift = (int)ctl[2];
     int64_t n = d_n ? (int64_t)*d_n : n_host;  // d_n: the compacted count (first pass)
     if (!kFirst) {
         if (ctl[1] <= (uint32_t)shift) return;  // constant digit: pass skipped
@@ -153,9 +157,11 @@ __global__ __launch_bounds__(256) void k_ds_scan(uint32_t *__restrict__ hist, in
                                                  uint32_t *__restrict__ ctl, int shift,
                                                  uint32_t *__restrict__ digit_total,
                                                  const uint32_t *__restrict__ d_n,
-                                                 unsigned long long *host_D, uint32_t tag) {
+                                                 unsigned long long *host_D, uint32_t tag,
+                                                 int msd) {
     __shared__ uint32_t s_sum[kScanGroups][kScanDigits];
     __shared__ uint32_t s_red[3][4];
+    if (kFirst && msd) shift = (int)ctl[2];
     int64_t n = d_n ? (int64_t)*d_n : n_host;
     if (!kFirst) {
         if (ctl[1] <= (uint32_t)shift) return;
@@ -257,26 +263,30 @@ __global__ __launch_bounds__(256) void k_ds_scan(uint32_t *__restrict__ hist, in
 // m &= ~(ballot(bit) ^ f), f = the lane's own bit sign-extended to a full mask (one v_bitop3
 // per 32-bit half); its rank is the count of those lanes below it, and every matching lane
 // stores the same new running count.
-template <int kBits>
-__device__ __forceinline__ int tile_rank_scatter(const uint32_t (&k)[kDIt],
-                                                 const uint32_t (&v)[kDIt], uint32_t keep,
+// kBits = 0: the digit width is the runtime rt_bits (1..6; one instantiation for every width).
+template <int kBits, int kIt = kDIt>
+__device__ __forceinline__ int tile_rank_scatter(const uint32_t (&k)[kIt],
+                                                 const uint32_t (&v)[kIt], uint32_t keep,
                                                  int shift, uint32_t *s_keys, uint32_t *s_vals,
-                                                 uint32_t *s_wcnt, uint32_t *s_tmp) {
+                                                 uint32_t *s_wcnt, uint32_t *s_tmp,
+                                                 int rt_bits = kBits) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    constexpr uint32_t kMask = (1u << kBits) - 1u;
+    const int nbits = kBits > 0 ? kBits : rt_bits;
+    const uint32_t kMask = (1u << nbits) - 1u;
     s_wcnt[tid] = 0u;
     __syncthreads();
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t *wcnt = s_wcnt + w * kDSubBins;
-    uint32_t rank[kDIt];
+    uint32_t rank[kIt];
 #pragma unroll
-    for (int j = 0; j < kDIt; ++j) {
+    for (int j = 0; j < kIt; ++j) {
         const bool kp = (keep >> j) & 1u;
         const uint32_t d = (k[j] >> shift) & kMask;
         const uint64_t m0 = __ballot(kp);
         uint32_t mlo = (uint32_t)m0, mhi = (uint32_t)(m0 >> 32);
 #pragma unroll
-        for (int b = 0; b < kBits; ++b) {
+        for (int b = 0; b < (kBits > 0 ? kBits : kDSub); ++b) {
+            if (kBits == 0 && b >= nbits) break;
             const uint32_t f = (uint32_t)(((int32_t)(d << (31 - b))) >> 31);
             const uint64_t bal = __ballot(f != 0u);
             mlo &= ~((uint32_t)bal ^ f);
@@ -296,7 +306,7 @@ __device__ __forceinline__ int tile_rank_scatter(const uint32_t (&k)[kDIt],
     s_wcnt[sw * kDSubBins + sd] = pre;
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kDIt; ++j) {
+    for (int j = 0; j < kIt; ++j) {
         if (!((keep >> j) & 1u)) continue;
         const uint32_t d = (k[j] >> shift) & kMask;
         const uint32_t pos = wcnt[d] + rank[j];
@@ -315,11 +325,12 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
     const void *__restrict__ in, uint2 *__restrict__ pairs_out, uint32_t *__restrict__ perm,
     int64_t n_host, int drop, const uint32_t *__restrict__ ctl, int shift,
     const uint32_t *__restrict__ hist, const uint32_t *__restrict__ digit_total,
-    const uint32_t *__restrict__ ids_in, const uint32_t *__restrict__ d_n) {
+    const uint32_t *__restrict__ ids_in, const uint32_t *__restrict__ d_n, int msd) {
     __shared__ uint32_t s_keys[kDT], s_vals[kDT], s_tab[kDBins];  // 48 KiB
     __shared__ uint32_t s_wcnt[kDSubBins * kDW];
     __shared__ uint32_t s_tmp[kDW];
     const uint32_t D = ctl[1];
+    if (kFirst && msd) shift = (int)ctl[2];
     int64_t n = d_n ? (int64_t)*d_n : n_host;
     if (!kFirst) {
         if (D <= (uint32_t)shift) return;
@@ -328,7 +339,9 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
     const int64_t base = (int64_t)blockIdx.x * kDT;
     if (base >= n) return;
     const int nbits = pass_bits(shift);
-    const bool last = shift + nbits >= 32 || D <= (uint32_t)(shift + nbits);
+    // msd: the pass sorted the top digit; it is the whole sort only when D <= 12
+    const bool last = (kFirst && msd) ? D <= (uint32_t)kDBits
+                                      : shift + nbits >= 32 || D <= (uint32_t)(shift + nbits);
     const uint32_t nbins = 1u << nbits, mask = nbins - 1u;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
 
@@ -482,6 +495,323 @@ __global__ __launch_bounds__(256) void k_ds_compact(const uint32_t *__restrict__
     }
 }
 
+// ---- MSD first pass + per-bucket local sort (the frame's depth sort, gsr_depth_sort_msd) -------
+// The LSD sort needs one up/scan/down pass per 12 key bits (two at C3, D = 24).  Here the one
+// global pass sorts the TOP 12 of the D varying bits (MSD: the keys land in 4096 buckets, each
+// bucket contiguous and stably ordered), and k_ds_local then sorts every bucket by the remaining
+// D - 12 bits in LDS -- one kernel instead of the second up/scan/down pass.  Buckets concatenated
+// in digit order, each sorted stably by its low bits, give the stable sort by the whole key.
+
+// D (the bits in which the kept keys differ) from the preprocess blocks' OR / AND of their kept
+// depth keys (GsrPreprocessArgs.block_pairs), as k_ds_scan derives it from the sort's own tiles:
+// ctl[1] = D, ctl[2] = the MSD pass's shift.  A kept key is a positive float's bits (depth >
+// 0.2), never 0, so OR == 0 means no kept key (D = 0).
+__global__ __launch_bounds__(1024) void k_ds_bits(const uint2 *__restrict__ keybits, int64_t nb,
+                                                  uint32_t *__restrict__ ctl) {
+    __shared__ uint32_t s_or[16], s_and[16];
+    uint32_t o = 0u, a = 0xFFFFFFFFu;
+    constexpr int kU = 8;  // loads in flight per thread
+    for (int64_t i0 = threadIdx.x; i0 < nb; i0 += kU * 1024) {
+        uint2 kb[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t i = i0 + (int64_t)u * 1024;
+            kb[u] = i < nb ? keybits[i] : make_uint2(0u, 0xFFFFFFFFu);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) o |= kb[u].x, a &= kb[u].y;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        o |= __shfl_xor(o, off);
+        a &= __shfl_xor(a, off);
+    }
+    if ((threadIdx.x & 63) == 0) s_or[threadIdx.x >> 6] = o, s_and[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        o = 0u, a = 0xFFFFFFFFu;
+        for (int i = 0; i < 16; ++i) o |= s_or[i], a &= s_and[i];
+        const uint32_t diff = o ? (o ^ a) : 0u;
+        const uint32_t D = diff ? 32u - (uint32_t)__clz(diff) : 0u;
+        ctl[1] = D;
+        ctl[2] = D > (uint32_t)kDBits ? D - (uint32_t)kDBits : 0u;
+    }
+}
+
+constexpr int kLGroup = kDW;                // buckets per k_ds_local block: one per wave
+constexpr int kLWave = 512;                 // keys a wave sorts alone (8 per lane)
+constexpr int kLIt = 8;                     // elements per lane of an in-LDS bucket sort
+constexpr int kLCap = kDThreads * kLIt;     // 4096 elements sorted in LDS at once
+constexpr int kLSub = kDSub;                // 6-bit sub-passes
+
+struct LocalSmem {
+    uint32_t keys[kLCap], vals[kLCap];
+    RadixTileSmem<kDW, kLIt> rt;  // 8-bit sub-passes (radix_tile_scatter, in LDS only)
+    uint32_t wcnt[kDSubBins * kDW];
+    uint32_t tmp[kDW];
+    uint32_t start[kLGroup + 1];  // the group's bucket starts (+ its end)
+    uint32_t base[kDSubBins], cstart[kDSubBins], ccount[kDSubBins];  // the slow path
+};
+
+// One sub-pass of `bits` (1..6) of the slow path's chunk ranking (runtime width).
+__device__ __forceinline__ int local_rank(const uint32_t (&k)[kLIt], const uint32_t (&v)[kLIt],
+                                          uint32_t keep, int shift, int bits, LocalSmem &sm) {
+    return tile_rank_scatter<0, kLIt>(k, v, keep, shift, sm.keys, sm.vals, sm.wcnt, sm.tmp, bits);
+}
+
+// Stable in-LDS sort of the n <= kLCap pairs at src[b0, b0 + n) -- consecutive buckets, already
+// in bucket order -- by the local key ((bucket - d0) << low) | (key & low mask) of `bits` bits,
+// in 8-bit sub-passes (radix_tile_scatter: element order wave, item, lane; elements past n carry
+// the largest key and sort last); the sorted ids go to perm[b0 ...].
+__device__ void local_sort_lds(const uint2 *__restrict__ src, uint32_t *__restrict__ perm,
+                               uint32_t b0, uint32_t n, uint32_t shift_hi, uint32_t d0, int low,
+                               int bits, LocalSmem &sm) {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t lmask = (1u << low) - 1u;
+    uint32_t k[kLIt], v[kLIt];
+#pragma unroll
+    for (int j = 0; j < kLIt; ++j) {
+        const uint32_t e = (uint32_t)(w * (kLCap / kDW) + j * 64 + lane);
+        k[j] = 0xFFFFFFFFu;
+        v[j] = 0u;
+        if (e < n) {
+            const uint2 q = src[b0 + e];
+            k[j] = ((((q.x >> shift_hi) & (kDBins - 1u)) - d0) << low) | (q.x & lmask);
+            v[j] = q.y;
+        }
+    }
+    for (int sh = 0; sh < bits; sh += 8) {
+        if (sh > 0) {  // reload the previous sub-pass's order (the first n entries)
+#pragma unroll
+            for (int j = 0; j < kLIt; ++j) {
+                const uint32_t p = (uint32_t)(w * (kLCap / kDW) + j * 64 + lane);
+                k[j] = p < n ? sm.keys[p] : 0xFFFFFFFFu;
+                v[j] = p < n ? sm.vals[p] : 0u;
+            }
+            __syncthreads();  // every lane holds its elements before the LDS is overwritten
+        }
+        radix_tile_scatter<kDW, kLIt, false, false>(k, v, (int)n, sh, min(8, bits - sh), nullptr,
+                                                    0, 0u, nullptr, nullptr, nullptr, sm.rt,
+                                                    sm.keys, sm.vals);
+    }
+    for (uint32_t i = tid; i < n; i += kDThreads) perm[b0 + i] = sm.vals[i];
+    __syncthreads();  // the LDS is reused by the caller's next sort
+}
+
+// The slow path for one bucket of n > kLCap pairs at src[b0 ...]: a stable LSD over its `low`
+// key bits in 6-bit sub-passes through global memory (ping-pong src <-> tmp at the same
+// offsets; the last sub-pass writes the ids to perm), the block walking the bucket in 4096-pair
+// chunks: count the digits, scan, then per chunk rank it in LDS and place every digit's run at
+// that digit's running offset.  Only a degenerate scene (more than 8192 kept Gaussians sharing
+// the top 12 of the varying depth bits) takes it.
+__device__ void local_sort_big(uint2 *__restrict__ src, uint2 *__restrict__ tmp,
+                               uint32_t *__restrict__ perm, uint32_t b0, uint32_t n, int low,
+                               LocalSmem &sm) {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    if (low == 0) {
+        for (uint32_t e = tid; e < n; e += kDThreads) perm[b0 + e] = src[b0 + e].y;
+        return;
+    }
+    uint2 *a = src, *b = tmp;
+    for (int sh = 0; sh < low; sh += kLSub) {
+        const int bits = min(kLSub, low - sh);
+        const uint32_t mask = (1u << bits) - 1u;
+        const bool last = sh + kLSub >= low;
+        if (tid < kDSubBins) sm.base[tid] = 0u;
+        __syncthreads();
+        for (uint32_t e = tid; e < n; e += kDThreads) atomicAdd(&sm.base[(a[b0 + e].x >> sh) & mask], 1u);
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t run = 0u;
+            for (int d = 0; d < kDSubBins; ++d) {
+                const uint32_t c = sm.base[d];
+                sm.base[d] = run;
+                run += c;
+            }
+        }
+        __syncthreads();
+        for (uint32_t c0 = 0; c0 < n; c0 += (uint32_t)kLCap) {
+            const uint32_t m = min((uint32_t)kLCap, n - c0);
+            uint32_t k[kLIt], v[kLIt], keep = 0u;
+#pragma unroll
+            for (int j = 0; j < kLIt; ++j) {
+                const uint32_t e = (uint32_t)(w * (kLCap / kDW) + j * 64 + lane);
+                k[j] = v[j] = 0u;
+                if (e < m) {
+                    const uint2 q = a[b0 + c0 + e];
+                    k[j] = q.x;
+                    v[j] = q.y;
+                    keep |= 1u << j;
+                }
+            }
+            const int kept = local_rank(k, v, keep, sh, bits, sm);
+            // the chunk's digit runs: start and count of every digit
+            if (tid < kDSubBins) sm.ccount[tid] = 0u;
+            __syncthreads();
+            for (int i = tid; i < kept; i += kDThreads) {
+                const uint32_t d = (sm.keys[i] >> sh) & mask;
+                if (i == 0 || ((sm.keys[i - 1] >> sh) & mask) != d) sm.cstart[d] = (uint32_t)i;
+                if (i == kept - 1 || ((sm.keys[i + 1] >> sh) & mask) != d)
+                    sm.ccount[d] = (uint32_t)i + 1u;  // end (count = end - start below)
+            }
+            __syncthreads();
+            for (int i = tid; i < kept; i += kDThreads) {
+                const uint32_t d = (sm.keys[i] >> sh) & mask;
+                const uint32_t g = sm.base[d] + ((uint32_t)i - sm.cstart[d]);
+                if (last)
+                    perm[b0 + g] = sm.vals[i];
+                else
+                    b[b0 + g] = make_uint2(sm.keys[i], sm.vals[i]);
+            }
+            __syncthreads();
+            if (tid < kDSubBins && sm.ccount[tid]) sm.base[tid] += sm.ccount[tid] - sm.cstart[tid];
+            __syncthreads();
+        }
+        uint2 *t = a;
+        a = b;
+        b = t;
+    }
+}
+
+// One wave sorts the n <= kLWave pairs of one bucket at src[b0 ...] by their low `low` key bits,
+// stably, alone: 8 pairs per lane (element j * 64 + lane), 6-bit sub-passes ranked with one
+// ballot per bit against a per-wave digit count in LDS (the lanes of a wave are in lockstep, so
+// no block barrier: the wavefront fences only keep the compiler from moving LDS accesses across
+// the hand-offs), scattered into the wave's LDS slice; the ids go to perm[b0 ...].
+__device__ void wave_sort_bucket(const uint2 *__restrict__ src, uint32_t *__restrict__ perm,
+                                 uint32_t b0, uint32_t n, int low, uint32_t *s_keys,
+                                 uint32_t *s_vals, uint32_t *cnt) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t lmask = (1u << low) - 1u;
+    constexpr int kIt = kLWave / 64;
+    uint32_t k[kIt], v[kIt];
+#pragma unroll
+    for (int j = 0; j < kIt; ++j) {
+        const uint32_t e = (uint32_t)(j * 64 + lane);
+        k[j] = v[j] = 0u;
+        if (e < n) {
+            const uint2 q = src[b0 + e];
+            k[j] = q.x & lmask;
+            v[j] = q.y;
+        }
+    }
+    for (int sh = 0; sh < low; sh += kDSub) {
+        const int bits = min(kDSub, low - sh);
+        const uint32_t mask = (1u << bits) - 1u;
+        cnt[lane] = 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t rank[kIt];
+#pragma unroll
+        for (int j = 0; j < kIt; ++j) {
+            const bool valid = (uint32_t)(j * 64 + lane) < n;
+            const uint32_t d = (k[j] >> sh) & mask;
+            const uint64_t m0 = __ballot(valid);
+            uint32_t mlo = (uint32_t)m0, mhi = (uint32_t)(m0 >> 32);
+#pragma unroll
+            for (int b = 0; b < kDSub; ++b) {
+                if (b >= bits) break;
+                const uint32_t f = (uint32_t)(((int32_t)(d << (31 - b))) >> 31);
+                const uint64_t bal = __ballot(f != 0u);
+                mlo &= ~((uint32_t)bal ^ f);
+                mhi &= ~((uint32_t)(bal >> 32) ^ f);
+            }
+            const uint64_t m = ((uint64_t)mhi << 32) | mlo;
+            const uint32_t prior = cnt[d];
+            rank[j] = prior + (uint32_t)__popcll(m & lt);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            if (valid) cnt[d] = prior + (uint32_t)__popcll(m);  // same value from every match
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        // exclusive scan of the 64 digit counts (one per lane)
+        const uint32_t c = cnt[lane];
+        const uint32_t ex = wave_inclusive_scan(c) - c;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        cnt[lane] = ex;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int j = 0; j < kIt; ++j) {
+            if ((uint32_t)(j * 64 + lane) >= n) continue;
+            const uint32_t pos = cnt[(k[j] >> sh) & mask] + rank[j];
+            s_keys[pos] = k[j];
+            s_vals[pos] = v[j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int j = 0; j < kIt; ++j) {
+            const uint32_t e = (uint32_t)(j * 64 + lane);
+            if (e < n) {
+                k[j] = s_keys[e];
+                v[j] = s_vals[e];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+#pragma unroll
+    for (int j = 0; j < kIt; ++j) {
+        const uint32_t e = (uint32_t)(j * 64 + lane);
+        if (e < n) perm[b0 + e] = v[j];
+    }
+}
+
+// Block g: buckets [8 g, 8 g + 8) of the MSD pass's output (pairs in bucket order; bucket d
+// starts at the exclusive sum of digit_total[0, d)), one per wave: a bucket of <= 512 keys (all
+// of them at C3, D = 24: at most ~500) is sorted by its wave alone; larger ones (4K frames: up
+// to ~2,800) by the whole block in LDS after the waves, in 8-bit sub-passes; past 4096 keys by
+// the slow path.  D <= 12: the MSD pass was the whole sort.
+__global__ __launch_bounds__(kDThreads) void k_ds_local(uint2 *__restrict__ pairs,
+                                                        uint2 *__restrict__ tmp,
+                                                        uint32_t *__restrict__ perm,
+                                                        const uint32_t *__restrict__ ctl,
+                                                        const uint32_t *__restrict__ digit_total) {
+    __shared__ LocalSmem sm;
+    const uint32_t D = ctl[1];
+    if (D <= (uint32_t)kDBits) return;
+    const int low = (int)(D - (uint32_t)kDBits);  // bits below the MSD digit
+    const uint32_t shift_hi = (uint32_t)low;
+    const int tid = threadIdx.x, w = tid >> 6;
+    const uint32_t d0 = blockIdx.x * kLGroup;
+    // the group's start: the digit totals before it (8 per thread, one block sum)
+    {
+        uint32_t acc = 0u;
+#pragma unroll
+        for (int i = 0; i < kDPer; ++i) {
+            const uint32_t d = (uint32_t)tid * kDPer + i;
+            acc += d < d0 ? digit_total[d] : 0u;
+        }
+        uint32_t total;
+        blockw_exclusive_scan<kDW>(acc, sm.tmp, total);
+        if (tid == 0) {
+            uint32_t run = total;
+            for (int i = 0; i < kLGroup; ++i) {
+                sm.start[i] = run;
+                run += digit_total[d0 + i];
+            }
+            sm.start[kLGroup] = run;
+        }
+        __syncthreads();
+    }
+    {
+        const uint32_t b0 = sm.start[w], bn = sm.start[w + 1] - b0;
+        if (bn > 0u && bn <= (uint32_t)kLWave)
+            wave_sort_bucket(pairs, perm, b0, bn, low, sm.keys + w * kLWave, sm.vals + w * kLWave,
+                             sm.wcnt + w * kDSubBins);
+    }
+    __syncthreads();
+    for (int i = 0; i < kLGroup; ++i) {  // the larger buckets, one at a time by the block
+        const uint32_t b0 = sm.start[i], bn = sm.start[i + 1] - b0;
+        if (bn <= (uint32_t)kLWave) continue;
+        if (bn <= (uint32_t)kLCap)
+            local_sort_lds(pairs, perm, b0, bn, shift_hi, d0 + (uint32_t)i, low, low, sm);
+        else
+            local_sort_big(pairs, tmp, perm, b0, bn, low, sm);
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 int64_t gsr_depth_sort_hist_words(int64_t n) {
@@ -508,18 +838,18 @@ static hipError_t ds_passes(const uint32_t *keys, const uint32_t *ids_in, const 
         const int shift = p * kDBits;
         if (p == 0) {
             hipLaunchKernelGGL(k_ds_upsweep<true>, dim3(nt), dim3(kDThreads), 0, s, in[p], n, drop,
-                               ctl, shift, hist, d_n);
+                               ctl, shift, hist, d_n, 0);
             hipLaunchKernelGGL(k_ds_scan<true>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist,
-                               n, ctl, shift, digit_total, d_n, host_D, tag);
+                               n, ctl, shift, digit_total, d_n, host_D, tag, 0);
             hipLaunchKernelGGL(k_ds_downsweep<true>, dim3(nt), dim3(kDThreads), 0, s, in[p], out[p],
-                               perm, n, drop, ctl, shift, hist, digit_total, ids_in, d_n);
+                               perm, n, drop, ctl, shift, hist, digit_total, ids_in, d_n, 0);
         } else {
             hipLaunchKernelGGL(k_ds_upsweep<false>, dim3(nt), dim3(kDThreads), 0, s, in[p], n, 0,
-                               ctl, shift, hist, nullptr);
+                               ctl, shift, hist, nullptr, 0);
             hipLaunchKernelGGL(k_ds_scan<false>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist,
-                               n, ctl, shift, digit_total, nullptr, nullptr, 0u);
+                               n, ctl, shift, digit_total, nullptr, nullptr, 0u, 0);
             hipLaunchKernelGGL(k_ds_downsweep<false>, dim3(nt), dim3(kDThreads), 0, s, in[p],
-                               out[p], perm, n, 0, ctl, shift, hist, digit_total, nullptr, nullptr);
+                               out[p], perm, n, 0, ctl, shift, hist, digit_total, nullptr, nullptr, 0);
         }
     }
     return hipGetLastError();
@@ -534,6 +864,25 @@ hipError_t gsr_depth_sort(const uint32_t *keys, int64_t n, int drop, uint2 *pair
         return hipErrorInvalidValue;
     return ds_passes(keys, nullptr, nullptr, n, drop, pairs_a, pairs_b, perm, hist, digit_total,
                      ctl, pass_begin, pass_end, host_D, tag, s);
+}
+
+hipError_t gsr_depth_sort_msd(const uint32_t *keys, int64_t n, const uint2 *keybits,
+                              int64_t n_keybits, uint2 *pairs_a, uint2 *pairs_b, uint32_t *perm,
+                              uint32_t *hist, uint32_t *digit_total, uint32_t *ctl, hipStream_t s,
+                              unsigned long long *host_D, uint32_t tag) {
+    if (n <= 0) return hipSuccess;
+    if (n > (int64_t)UINT32_MAX) return hipErrorInvalidValue;
+    const unsigned nt = (unsigned)((n + kDT - 1) / kDT);
+    hipLaunchKernelGGL(k_ds_bits, dim3(1), dim3(1024), 0, s, keybits, n_keybits, ctl);
+    hipLaunchKernelGGL(k_ds_upsweep<true>, dim3(nt), dim3(kDThreads), 0, s, keys, n, 1, ctl, 0,
+                       hist, nullptr, 1);
+    hipLaunchKernelGGL(k_ds_scan<true>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist, n, ctl,
+                       0, digit_total, nullptr, host_D, tag, 1);
+    hipLaunchKernelGGL(k_ds_downsweep<true>, dim3(nt), dim3(kDThreads), 0, s, keys, pairs_a, perm,
+                       n, 1, ctl, 0, hist, digit_total, nullptr, nullptr, 1);
+    hipLaunchKernelGGL(k_ds_local, dim3(kDBins / kLGroup), dim3(kDThreads), 0, s, pairs_a, pairs_b,
+                       perm, ctl, digit_total);
+    return hipGetLastError();
 }
 
 hipError_t gsr_depth_sort_compacted(const uint32_t *keys, int64_t n, uint32_t *block_kept,

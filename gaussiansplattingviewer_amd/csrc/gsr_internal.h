@@ -317,6 +317,15 @@ hipError_t gsr_depth_sort(const uint32_t *keys, int64_t n, int drop, uint2 *pair
                           uint2 *pairs_b, uint32_t *perm, uint32_t *hist, uint32_t *digit_total,
                           uint32_t *ctl, int pass_begin, int pass_end, hipStream_t s,
                           unsigned long long *host_D = nullptr, uint32_t tag = 0);
+// The frame's sort (no compaction): D from the preprocess blocks' OR / AND of their kept keys
+// (keybits: n_keybits uint2, GsrPreprocessArgs.block_pairs after the counts), one global pass
+// over the top 12 of the D varying bits (dropping the 0xFFFFFFFF keys), then every bucket sorted
+// by the remaining bits in LDS.  Same result, ctl and perm contract as gsr_depth_sort with drop;
+// pairs_a holds the bucketed pairs, pairs_b is scratch.  host_D as in gsr_depth_sort.
+hipError_t gsr_depth_sort_msd(const uint32_t *keys, int64_t n, const uint2 *keybits,
+                              int64_t n_keybits, uint2 *pairs_a, uint2 *pairs_b, uint32_t *perm,
+                              uint32_t *hist, uint32_t *digit_total, uint32_t *ctl, hipStream_t s,
+                              unsigned long long *host_D = nullptr, uint32_t tag = 0);
 // Compacting front end for sparse key sets (strips): the kept keys of each 256-key block
 // (block_kept[b] of them, from the preprocess) are written in order to keys_c, their indices
 // to ids_c, and their count to ctl[0]; then the sort runs on those (gsr_depth_sort_compacted,

@@ -40,7 +40,8 @@ extern "C" {
 #endif
 
 /* 2 (round 4): option ids renumbered (GSR_OPT_COLUMN_PAIRS retired, tight binning moved to 13,
- * ids 10 and 12 reserved), gsr_get_binning exports tight lists. */
+ * ids 10 and 12 reserved), GSR_OPT_DEPTH_SORT (id 11, was COMPACT_SORT) gains the MSD form,
+ * gsr_get_binning exports tight lists. */
 #define GSR_ABI_VERSION 2
 
 enum {
@@ -213,10 +214,12 @@ const char *gsr_stage_name(int i);
  *   GSR_OPT_BLEND_FAST (default 1): blend arithmetic with log2(e) folded into the conic, FMA
  *     contraction and the hardware exp2 (tolerance in tests/gpu_helpers.py); 0 keeps upstream's
  *     per-pixel operation order (IEEE, no FMA, ocml expf).
- *   GSR_OPT_COMPACT_SORT (default -1 = auto): 1 = the depth sort first compacts the keys of the
- *     Gaussians with pairs in the strip and sorts only those; 0 = its first pass drops the others
- *     while it sorts; auto = compact on strips (a proper subset of the tile rows) of >= 4M
- *     Gaussians.
+ *   GSR_OPT_DEPTH_SORT (default -1 = auto): the form of the per-frame depth sort.  0 = LSD passes
+ *     of 12 key bits, the first dropping the keys of Gaussians without pairs in the strip;
+ *     1 = the same after a compaction of the kept keys; 2 = one MSD pass over the top 12 of the
+ *     bits in which the kept keys differ, then every bucket sorted by the rest in LDS.  auto =
+ *     1 on strips (a proper subset of the tile rows) of >= 4M Gaussians, else 2 when the
+ *     previous frame's kept keys differed in <= 24 bits, else 0.
  *   GSR_OPT_TIGHT_BINNING (default 1): with the column-first form and no n_contrib output, each
  *     Gaussian of a rect up to 8 tile columns x 15 rows is paired only with the tiles its
  *     alpha >= 1/255 ellipse reaches (upstream's blend skips it on the others), so the lists are
@@ -228,7 +231,7 @@ const char *gsr_stage_name(int i);
  * tile column) segments, the second on packed (tile row, Gaussian id) words) up to 256 tile
  * columns and strip rows, else the per-pair form; both produce the same lists.  Ids 10 and 12
  * are retired (ABI 1's column-pairs and tight-binning options) and rejected. */
-enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_COMPACT_SORT = 11,
+enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_DEPTH_SORT = 11,
        GSR_OPT_TIGHT_BINNING = 13 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
 

@@ -284,7 +284,9 @@ def test_headline_config_c3(gpu, c3_oracle, fast):
 
 VARIANTS = {  # [(option, alternative value, default), ...]
     "no_cull": [(_lib.GSR_OPT_BLEND_CULL, 0, 1)],
-    "compact_sort": [(_lib.GSR_OPT_COMPACT_SORT, 1, -1)],
+    "lsd_sort": [(_lib.GSR_OPT_DEPTH_SORT, 0, -1)],
+    "compact_sort": [(_lib.GSR_OPT_DEPTH_SORT, 1, -1)],
+    "msd_sort": [(_lib.GSR_OPT_DEPTH_SORT, 2, -1)],
 }
 
 
@@ -321,7 +323,7 @@ def test_sort_implementations_agree(gpu, variant, size):
         np.testing.assert_array_equal(alt[k], ref[k], err_msg=k)
 
 
-@pytest.mark.parametrize("variant", ["default", "per_pair", "compact_sort"])
+@pytest.mark.parametrize("variant", ["default", "per_pair", "lsd_sort", "compact_sort", "msd_sort"])
 def test_long_tile_lists_and_depth_ties(gpu, oracle_mod, variant):
     """Tiles covered by more than 2048 splats (multi-chunk digit runs in the tile sort, long
     blend lists) and half of the Gaussians at one depth (ties: upstream orders them by
@@ -340,18 +342,19 @@ def test_long_tile_lists_and_depth_ties(gpu, oracle_mod, variant):
     assert_parity(hip, orc)
 
 
-@pytest.mark.parametrize("compact", [0, 1])
+@pytest.mark.parametrize("form", [0, 1, 2])
 @pytest.mark.parametrize("spread", [0.0, 2e-4, 0.05, 1.5, 60.0])
-def test_depth_sort_pass_regimes(gpu, oracle_mod, spread, compact):
+def test_depth_sort_pass_regimes(gpu, oracle_mod, spread, form):
     """The depth sort (depth_sort.hip) sorts only the key bits that differ between the kept
-    Gaussians' depths (D = bits of OR ^ AND), in 12-bit passes decided on the device: all
-    depths equal (D = 0), within 2^12 ulps (one pass), within 2^24 (two passes: 2.5..2.55, and
-    2.5..4 across a float exponent) and 2.5..62.5 (three passes, five exponents).  25k Gaussians
-    = 4 sort tiles; off-screen ones are dropped by pass 0 (sentinel keys), or compacted away
-    first (GSR_OPT_COMPACT_SORT)."""
+    Gaussians' depths (D = bits of OR ^ AND): all depths equal (D = 0), within 2^12 ulps, within
+    2^24 (2.5..2.55, and 2.5..4 across a float exponent) and 2.5..62.5 (five exponents, D > 24).
+    25k Gaussians = 4 sort tiles; off-screen ones are dropped.  GSR_OPT_DEPTH_SORT forms: 0 LSD
+    passes of 12 bits decided on the device, 1 the same after compacting the kept keys, 2 one MSD
+    pass over the top 12 of the D bits then every bucket sorted in LDS (its slow path for buckets
+    past 4096 keys included: at D <= 12 or with few distinct depths the buckets are crowded)."""
     g = synthetic_gaussians(25000, 3, 31)
     rng = np.random.default_rng(31)
-    _set_option(gpu, _lib.GSR_OPT_COMPACT_SORT, compact)
+    _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, form)
     g.xyz[:, 2] = (np.float32(0.5) - rng.random(25000, dtype=np.float32) * np.float32(spread))
     g.xyz[::5, 2] = g.xyz[1::5, 2]  # ties across tiles
     s = scene_inputs(g, static_camera(320, 240, (0, 0, 3.0)), 3)
@@ -360,7 +363,32 @@ def test_depth_sort_pass_regimes(gpu, oracle_mod, spread, compact):
     try:
         hip = run_hip(s, gpu)
     finally:
-        _set_option(gpu, _lib.GSR_OPT_COMPACT_SORT, -1)
+        _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, -1)
+    assert_parity(hip, orc)
+
+
+@pytest.mark.parametrize("n", [5000, 60000])
+def test_msd_sort_crowded_bucket(gpu, oracle_mod, n):
+    """The MSD sort's slow path: most kept Gaussians in one bucket of the top 12 varying key bits
+    (depths within 2^-13 relative of each other, a few far ones widen D to 24), so one bucket
+    holds more keys than the in-LDS sort (4096) and the block sorts it through global memory."""
+    g = synthetic_gaussians(n, 3, 33)
+    rng = np.random.default_rng(33)
+    g.xyz[:, :2] = rng.uniform(-0.5, 0.5, (n, 2)).astype(np.float32)  # all in view
+    g.xyz[:, 2] = np.float32(0.5) + rng.random(n, dtype=np.float32) * np.float32(1e-4)
+    g.xyz[:50, 2] = np.float32(-1.5)  # widen the key bits
+    g.scale[:] = np.float32(0.01)
+    s = scene_inputs(g, static_camera(320, 240, (0, 0, 3.0)), 3)
+    orc = run_oracle(oracle_mod, s)
+    d = orc["depths"][orc["radii"] > 0].view(np.uint32)
+    D = int(np.bitwise_or.reduce(d) ^ np.bitwise_and.reduce(d)).bit_length()
+    top = (d >> np.uint32(D - 12)) & np.uint32(4095)
+    assert D == 24 and np.bincount(top).max() > 4096, (D, np.bincount(top).max())
+    _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, 2)
+    try:
+        hip = run_hip(s, gpu)
+    finally:
+        _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, -1)
     assert_parity(hip, orc)
 
 
@@ -373,7 +401,7 @@ def test_tile_lists_of_one_depth(gpu, oracle_mod):
 
 
 def test_compacted_strip_colour_path(gpu):
-    """Compacted strip frames (GSR_OPT_COMPACT_SORT: auto on strips of >= 4M Gaussians, forced
+    """Compacted strip frames (GSR_OPT_DEPTH_SORT 1: auto on strips of >= 4M Gaussians, forced
     here) colour only the compacted kept ids (k_color_ids, handed from the main stream's
     compaction to the second stream by an event) when no rgb output is requested -- the bench's
     and the viewer's call.  Every strip must be bit-identical to the same rows of the full frame
@@ -384,7 +412,7 @@ def test_compacted_strip_colour_path(gpu):
     pix = ("final_T", "n_contrib")  # no "rgb": the compacted-id colour pass is allowed
     full = run_hip(s, gpu, extras=pix)
     gy = (H + 15) // 16
-    _set_option(gpu, _lib.GSR_OPT_COMPACT_SORT, 1)
+    _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, 1)
     try:
         for r in range(8):
             rows = strip_rows(gy, 8, r)
@@ -398,4 +426,4 @@ def test_compacted_strip_colour_path(gpu):
             for k in ("color", "final_T", "n_contrib", "point_list"):
                 np.testing.assert_array_equal(lean[k], part[k], err_msg=k)
     finally:
-        _set_option(gpu, _lib.GSR_OPT_COMPACT_SORT, -1)
+        _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, -1)
