@@ -191,7 +191,9 @@ hipError_t gsr_launch_digit_scan_n(uint32_t *hist, int64_t nb, uint32_t *digit_t
 }
 
 namespace {
-constexpr int kSW = 8, kSIt = 8;  // sort tile: 8 waves x 8 keys per lane
+// sort tile: 8 waves x 8 keys per lane (4096 keys; 8 x 16 and 16 x 16 measured no faster at 4K
+// and slower at C3, profiles/r04o_ab_rs_tile.txt)
+constexpr int kSW = 8, kSIt = 8;
 constexpr int64_t kST = (int64_t)kSW * 64 * kSIt;
 }  // namespace
 
