@@ -77,7 +77,7 @@ def parse():
     ap.add_argument("--inflight", type=int, default=2,
                     help="frames in flight (FramePipeline: own stream + context slot each); "
                          "1 = serial forwards")
-    ap.add_argument("--depth-sort", default="auto", choices=["auto", "lsd", "compact", "msd"],
+    ap.add_argument("--depth-sort", default="auto", choices=["auto", "lsd", "compact", "msd", "compact-msd"],
                     help="GSR_OPT_DEPTH_SORT: LSD passes, LSD after compacting the kept keys, or "
                          "the MSD pass + per-bucket local sort (auto: compact on strips of >= 4M "
                          "Gaussians, else MSD when the last frame's depth keys differed in <= 24 "
@@ -388,7 +388,7 @@ def main():
         opt = lambda o, v: _lib.check(lib.gsr_set_option(c, o, v), "gsr_set_option")  # noqa: E731
         opt(_lib.GSR_OPT_BLEND_FAST, {"exact": 0, "fast": 1}[args.blend])
         opt(_lib.GSR_OPT_DEPTH_SORT,
-            {"auto": -1, "lsd": 0, "compact": 1, "msd": 2}[args.depth_sort])
+            {"auto": -1, "lsd": 0, "compact": 1, "msd": 2, "compact-msd": 3}[args.depth_sort])
 
     # The untimed diagnostic passes run first, so the device has been rendering for ~200 frames
     # when the timed region starts: a run of 20 timed frames after 5 warmup frames measured

@@ -366,15 +366,15 @@ int setup_frame(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     pa.records = static_cast<gsr::SplatRecord *>(ctx->records.p);
     pa.sort_keys = static_cast<uint32_t *>(ctx->sort_keys.p);
     f.compact_sort = ctx->depth_sort < 0 ? (f.rows_tiles < f.gy && P >= kCompactP)
-                                         : ctx->depth_sort == 1;
+                                         : ctx->depth_sort == 1 || ctx->depth_sort == 3;
     pa.block_kept = f.compact_sort ? static_cast<uint32_t *>(ctx->block_kept.p) : nullptr;
     // the MSD sort wants buckets of a few thousand keys: its 4096 buckets split the top 12 of the
     // D varying key bits, which balances them when D <= 24 (depths within one or two float
     // exponents, C2-C5).  Wider spreads (the clustered c3r, D = 31) crowd some buckets past the
     // LDS sort, so they keep the LSD passes; the choice follows the previous frame's D (the
     // result is the same either way, only the time differs)
-    f.msd_sort = ctx->depth_sort < 0 ? !f.compact_sort && ctx->last_D <= (uint32_t)kMsdMaxD
-                                     : ctx->depth_sort == 2;
+    f.msd_sort = ctx->depth_sort < 0 ? ctx->last_D <= (uint32_t)kMsdMaxD
+                                     : ctx->depth_sort >= 2;
     pa.strip_rect = static_cast<uint2 *>(ctx->strip_rect.p);
     // tight binning: the column-first form, and no n_contrib (upstream's n_contrib counts list
     // positions of the full 3-sigma pairs); span words only then (NULL: every rect full).  Full
@@ -409,22 +409,24 @@ int launch_depth_sort(gsr_context *ctx, const Frame &f, int p0, int p1) {
     uint32_t *perm = static_cast<uint32_t *>(ctx->perm.p);
     uint2 *ds_a = static_cast<uint2 *>(ctx->ds_a.p), *ds_b = static_cast<uint2 *>(ctx->ds_b.p);
     hipError_t e;
+    const int64_t nb = (f.P + 255) / 256;  // preprocess blocks (their key OR / AND words)
+    const uint2 *keybits = reinterpret_cast<const uint2 *>(f.pa.block_pairs + nb);
     if (f.compact_sort) {
-        // the compacted keys / ids live in ds_b until pass 1 overwrites it
+        // the compacted keys / ids live in ds_b until pass 1 (or the MSD pass) has read them
+        if (f.msd_sort && p0 != 0) return GSR_OK;  // (no later passes)
         uint32_t *keys_c = reinterpret_cast<uint32_t *>(ds_b), *ids_c = keys_c + f.P;
         e = gsr_depth_sort_compacted(f.pa.sort_keys, f.P, f.pa.block_kept, keys_c, ids_c, ds_a,
                                      ds_b, perm, hist, digit_total, ctl, p0, p1, f.s,
                                      ctx->d_hostD, f.tag,
                                      f.color_ids ? static_cast<uint32_t *>(ctx->color_ids.p)
                                                  : nullptr,
-                                     f.color_ids ? ctx->compacted : nullptr);
+                                     f.color_ids ? ctx->compacted : nullptr,
+                                     f.msd_sort ? keybits : nullptr, nb);
     } else if (f.msd_sort) {
         // MSD pass + per-bucket local sort, the whole sort at once (D from the preprocess blocks)
         if (p0 != 0) return GSR_OK;  // (no later passes)
-        const int64_t nb = (f.P + 255) / 256;
-        e = gsr_depth_sort_msd(f.pa.sort_keys, f.P,
-                               reinterpret_cast<const uint2 *>(f.pa.block_pairs + nb), nb, ds_a,
-                               ds_b, perm, hist, digit_total, ctl, f.s, ctx->d_hostD, f.tag);
+        e = gsr_depth_sort_msd(f.pa.sort_keys, f.P, keybits, nb, ds_a, ds_b, perm, hist,
+                               digit_total, ctl, f.s, ctx->d_hostD, f.tag);
     } else {
         e = gsr_depth_sort(f.pa.sort_keys, f.P, 1, ds_a, ds_b, perm, hist, digit_total, ctl, p0,
                            p1, f.s, ctx->d_hostD, f.tag);
@@ -828,8 +830,8 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
             return GSR_OK;
         case GSR_OPT_TIGHT_BINNING: ctx->tight = value ? 1 : 0; return GSR_OK;
         case GSR_OPT_DEPTH_SORT:
-            if (value < -1 || value > 2)
-                return fail(GSR_E_INVALID, "gsr_set_option: depth sort -1..2");
+            if (value < -1 || value > 3)
+                return fail(GSR_E_INVALID, "gsr_set_option: depth sort -1..3");
             ctx->depth_sort = (int)value;
             return GSR_OK;
         default:

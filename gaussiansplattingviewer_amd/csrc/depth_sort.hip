@@ -866,22 +866,32 @@ hipError_t gsr_depth_sort(const uint32_t *keys, int64_t n, int drop, uint2 *pair
                      ctl, pass_begin, pass_end, host_D, tag, s);
 }
 
+// The MSD form over keys (drop: the kDropKey ones are dropped) or over compacted keys / ids_in
+// whose count is *d_n (grids sized for n).
+static void msd_launch(const uint32_t *keys, const uint32_t *ids_in, const uint32_t *d_n, int drop,
+                       int64_t n, const uint2 *keybits, int64_t n_keybits, uint2 *pairs_a,
+                       uint2 *pairs_b, uint32_t *perm, uint32_t *hist, uint32_t *digit_total,
+                       uint32_t *ctl, hipStream_t s, unsigned long long *host_D, uint32_t tag) {
+    const unsigned nt = (unsigned)((n + kDT - 1) / kDT);
+    hipLaunchKernelGGL(k_ds_bits, dim3(1), dim3(1024), 0, s, keybits, n_keybits, ctl);
+    hipLaunchKernelGGL(k_ds_upsweep<true>, dim3(nt), dim3(kDThreads), 0, s, keys, n, drop, ctl, 0,
+                       hist, d_n, 1);
+    hipLaunchKernelGGL(k_ds_scan<true>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist, n, ctl,
+                       0, digit_total, d_n, host_D, tag, 1);
+    hipLaunchKernelGGL(k_ds_downsweep<true>, dim3(nt), dim3(kDThreads), 0, s, keys, pairs_a, perm,
+                       n, drop, ctl, 0, hist, digit_total, ids_in, d_n, 1);
+    hipLaunchKernelGGL(k_ds_local, dim3(kDBins / kLGroup), dim3(kDThreads), 0, s, pairs_a, pairs_b,
+                       perm, ctl, digit_total);
+}
+
 hipError_t gsr_depth_sort_msd(const uint32_t *keys, int64_t n, const uint2 *keybits,
                               int64_t n_keybits, uint2 *pairs_a, uint2 *pairs_b, uint32_t *perm,
                               uint32_t *hist, uint32_t *digit_total, uint32_t *ctl, hipStream_t s,
                               unsigned long long *host_D, uint32_t tag) {
     if (n <= 0) return hipSuccess;
     if (n > (int64_t)UINT32_MAX) return hipErrorInvalidValue;
-    const unsigned nt = (unsigned)((n + kDT - 1) / kDT);
-    hipLaunchKernelGGL(k_ds_bits, dim3(1), dim3(1024), 0, s, keybits, n_keybits, ctl);
-    hipLaunchKernelGGL(k_ds_upsweep<true>, dim3(nt), dim3(kDThreads), 0, s, keys, n, 1, ctl, 0,
-                       hist, nullptr, 1);
-    hipLaunchKernelGGL(k_ds_scan<true>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist, n, ctl,
-                       0, digit_total, nullptr, host_D, tag, 1);
-    hipLaunchKernelGGL(k_ds_downsweep<true>, dim3(nt), dim3(kDThreads), 0, s, keys, pairs_a, perm,
-                       n, 1, ctl, 0, hist, digit_total, nullptr, nullptr, 1);
-    hipLaunchKernelGGL(k_ds_local, dim3(kDBins / kLGroup), dim3(kDThreads), 0, s, pairs_a, pairs_b,
-                       perm, ctl, digit_total);
+    msd_launch(keys, nullptr, nullptr, 1, n, keybits, n_keybits, pairs_a, pairs_b, perm, hist,
+               digit_total, ctl, s, host_D, tag);
     return hipGetLastError();
 }
 
@@ -890,7 +900,8 @@ hipError_t gsr_depth_sort_compacted(const uint32_t *keys, int64_t n, uint32_t *b
                                     uint2 *pairs_b, uint32_t *perm, uint32_t *hist,
                                     uint32_t *digit_total, uint32_t *ctl, int pass_begin,
                                     int pass_end, hipStream_t s, unsigned long long *host_D,
-                                    uint32_t tag, uint32_t *ids_copy, hipEvent_t compacted) {
+                                    uint32_t tag, uint32_t *ids_copy, hipEvent_t compacted,
+                                    const uint2 *keybits, int64_t n_keybits) {
     if (n <= 0 || pass_begin >= pass_end) return hipSuccess;
     if (n > (int64_t)UINT32_MAX || pass_begin < 0 || pass_end > kDPasses)
         return hipErrorInvalidValue;
@@ -905,6 +916,14 @@ hipError_t gsr_depth_sort_compacted(const uint32_t *keys, int64_t n, uint32_t *b
         }
     }
     // the passes read the compacted count from ctl[0] (grids sized for n)
+    if (keybits) {  // the MSD form, the whole sort at once (pass_begin 0 only)
+        if (pass_begin != 0) return hipErrorInvalidValue;
+        // (pairs_b holds keys_c / ids_c: only the slow local sort of a degenerate bucket uses it,
+        // after the MSD pass has read them)
+        msd_launch(keys_c, ids_c, ctl, 0, n, keybits, n_keybits, pairs_a, pairs_b, perm, hist,
+                   digit_total, ctl, s, host_D, tag);
+        return hipGetLastError();
+    }
     return ds_passes(keys_c, ids_c, ctl, n, 0, pairs_a, pairs_b, perm, hist, digit_total, ctl,
                      pass_begin, pass_end, host_D, tag, s);
 }

@@ -330,14 +330,17 @@ hipError_t gsr_depth_sort_msd(const uint32_t *keys, int64_t n, const uint2 *keyb
 // (block_kept[b] of them, from the preprocess) are written in order to keys_c, their indices
 // to ids_c, and their count to ctl[0]; then the sort runs on those (gsr_depth_sort_compacted,
 // same contract as gsr_depth_sort with drop, n the uncompacted upper bound).  block_kept is
-// scanned in place.  keys_c / ids_c may be the two halves of pairs_b.
+// scanned in place.  keys_c / ids_c may be the two halves of pairs_b.  keybits (the preprocess
+// blocks' key OR / AND, as gsr_depth_sort_msd): the MSD form on the compacted keys instead of
+// the LSD passes (the whole sort in one call, pass_begin 0).
 hipError_t gsr_depth_sort_compacted(const uint32_t *keys, int64_t n, uint32_t *block_kept,
                                     uint32_t *keys_c, uint32_t *ids_c, uint2 *pairs_a,
                                     uint2 *pairs_b, uint32_t *perm, uint32_t *hist,
                                     uint32_t *digit_total, uint32_t *ctl, int pass_begin,
                                     int pass_end, hipStream_t s,
                                     unsigned long long *host_D = nullptr, uint32_t tag = 0,
-                                    uint32_t *ids_copy = nullptr, hipEvent_t compacted = nullptr);
+                                    uint32_t *ids_copy = nullptr, hipEvent_t compacted = nullptr,
+                                    const uint2 *keybits = nullptr, int64_t n_keybits = 0);
 
 // Binning: offsets scan over depth-sorted strip tile counts, duplicate into (tile, id)
 // pairs, and tile ranges.

@@ -217,9 +217,10 @@ const char *gsr_stage_name(int i);
  *   GSR_OPT_DEPTH_SORT (default -1 = auto): the form of the per-frame depth sort.  0 = LSD passes
  *     of 12 key bits, the first dropping the keys of Gaussians without pairs in the strip;
  *     1 = the same after a compaction of the kept keys; 2 = one MSD pass over the top 12 of the
- *     bits in which the kept keys differ, then every bucket sorted by the rest in LDS.  auto =
- *     1 on strips (a proper subset of the tile rows) of >= 4M Gaussians, else 2 when the
- *     previous frame's kept keys differed in <= 24 bits, else 0.
+ *     bits in which the kept keys differ, then every bucket sorted by the rest in LDS; 3 = 2
+ *     after the compaction.  auto = the compaction on strips (a proper subset of the tile rows)
+ *     of >= 4M Gaussians, the MSD form when the previous frame's kept keys differed in <= 24
+ *     bits (3 or 2), else the LSD passes (1 or 0).  Every form gives the same permutation.
  *   GSR_OPT_TIGHT_BINNING (default 1): with the column-first form and no n_contrib output, each
  *     Gaussian of a rect up to 8 tile columns x 15 rows is paired only with the tiles its
  *     alpha >= 1/255 ellipse reaches (upstream's blend skips it on the others), so the lists are

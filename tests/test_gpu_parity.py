@@ -287,6 +287,7 @@ VARIANTS = {  # [(option, alternative value, default), ...]
     "lsd_sort": [(_lib.GSR_OPT_DEPTH_SORT, 0, -1)],
     "compact_sort": [(_lib.GSR_OPT_DEPTH_SORT, 1, -1)],
     "msd_sort": [(_lib.GSR_OPT_DEPTH_SORT, 2, -1)],
+    "compact_msd": [(_lib.GSR_OPT_DEPTH_SORT, 3, -1)],
 }
 
 
@@ -323,7 +324,8 @@ def test_sort_implementations_agree(gpu, variant, size):
         np.testing.assert_array_equal(alt[k], ref[k], err_msg=k)
 
 
-@pytest.mark.parametrize("variant", ["default", "per_pair", "lsd_sort", "compact_sort", "msd_sort"])
+@pytest.mark.parametrize("variant", ["default", "per_pair", "lsd_sort", "compact_sort", "msd_sort",
+                                     "compact_msd"])
 def test_long_tile_lists_and_depth_ties(gpu, oracle_mod, variant):
     """Tiles covered by more than 2048 splats (multi-chunk digit runs in the tile sort, long
     blend lists) and half of the Gaussians at one depth (ties: upstream orders them by
@@ -342,7 +344,7 @@ def test_long_tile_lists_and_depth_ties(gpu, oracle_mod, variant):
     assert_parity(hip, orc)
 
 
-@pytest.mark.parametrize("form", [0, 1, 2])
+@pytest.mark.parametrize("form", [0, 1, 2, 3])
 @pytest.mark.parametrize("spread", [0.0, 2e-4, 0.05, 1.5, 60.0])
 def test_depth_sort_pass_regimes(gpu, oracle_mod, spread, form):
     """The depth sort (depth_sort.hip) sorts only the key bits that differ between the kept
@@ -351,7 +353,8 @@ def test_depth_sort_pass_regimes(gpu, oracle_mod, spread, form):
     25k Gaussians = 4 sort tiles; off-screen ones are dropped.  GSR_OPT_DEPTH_SORT forms: 0 LSD
     passes of 12 bits decided on the device, 1 the same after compacting the kept keys, 2 one MSD
     pass over the top 12 of the D bits then every bucket sorted in LDS (its slow path for buckets
-    past 4096 keys included: at D <= 12 or with few distinct depths the buckets are crowded)."""
+    past 4096 keys included: at D <= 12 or with few distinct depths the buckets are crowded), 3
+    the MSD form on the compacted keys."""
     g = synthetic_gaussians(25000, 3, 31)
     rng = np.random.default_rng(31)
     _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, form)
@@ -367,8 +370,9 @@ def test_depth_sort_pass_regimes(gpu, oracle_mod, spread, form):
     assert_parity(hip, orc)
 
 
+@pytest.mark.parametrize("form", [2, 3])
 @pytest.mark.parametrize("n", [5000, 60000])
-def test_msd_sort_crowded_bucket(gpu, oracle_mod, n):
+def test_msd_sort_crowded_bucket(gpu, oracle_mod, n, form):
     """The MSD sort's slow path: most kept Gaussians in one bucket of the top 12 varying key bits
     (depths within 2^-13 relative of each other, a few far ones widen D to 24), so one bucket
     holds more keys than the in-LDS sort (4096) and the block sorts it through global memory."""
@@ -384,7 +388,7 @@ def test_msd_sort_crowded_bucket(gpu, oracle_mod, n):
     D = int(np.bitwise_or.reduce(d) ^ np.bitwise_and.reduce(d)).bit_length()
     top = (d >> np.uint32(D - 12)) & np.uint32(4095)
     assert D == 24 and np.bincount(top).max() > 4096, (D, np.bincount(top).max())
-    _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, 2)
+    _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, form)
     try:
         hip = run_hip(s, gpu)
     finally:
@@ -400,9 +404,10 @@ def test_tile_lists_of_one_depth(gpu, oracle_mod):
     assert_parity(run_hip(s, gpu), run_oracle(oracle_mod, s))
 
 
-def test_compacted_strip_colour_path(gpu):
-    """Compacted strip frames (GSR_OPT_DEPTH_SORT 1: auto on strips of >= 4M Gaussians, forced
-    here) colour only the compacted kept ids (k_color_ids, handed from the main stream's
+@pytest.mark.parametrize("form", [1, 3])
+def test_compacted_strip_colour_path(gpu, form):
+    """Compacted strip frames (GSR_OPT_DEPTH_SORT 1 or 3: auto on strips of >= 4M Gaussians,
+    forced here, with the LSD passes or the MSD form) colour only the compacted kept ids (k_color_ids, handed from the main stream's
     compaction to the second stream by an event) when no rgb output is requested -- the bench's
     and the viewer's call.  Every strip must be bit-identical to the same rows of the full frame
     rendered without compaction (k_color over every Gaussian)."""
@@ -412,7 +417,7 @@ def test_compacted_strip_colour_path(gpu):
     pix = ("final_T", "n_contrib")  # no "rgb": the compacted-id colour pass is allowed
     full = run_hip(s, gpu, extras=pix)
     gy = (H + 15) // 16
-    _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, 1)
+    _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, form)
     try:
         for r in range(8):
             rows = strip_rows(gy, 8, r)
