@@ -873,7 +873,8 @@ static void msd_launch(const uint32_t *keys, const uint32_t *ids_in, const uint3
                        uint2 *pairs_b, uint32_t *perm, uint32_t *hist, uint32_t *digit_total,
                        uint32_t *ctl, hipStream_t s, unsigned long long *host_D, uint32_t tag) {
     const unsigned nt = (unsigned)((n + kDT - 1) / kDT);
-    hipLaunchKernelGGL(k_ds_bits, dim3(1), dim3(1024), 0, s, keybits, n_keybits, ctl);
+    if (keybits)  // (else ctl[1], ctl[2] are set: gsr_launch_count_pairs on this stream)
+        hipLaunchKernelGGL(k_ds_bits, dim3(1), dim3(1024), 0, s, keybits, n_keybits, ctl);
     hipLaunchKernelGGL(k_ds_upsweep<true>, dim3(nt), dim3(kDThreads), 0, s, keys, n, drop, ctl, 0,
                        hist, d_n, 1);
     hipLaunchKernelGGL(k_ds_scan<true>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist, n, ctl,
@@ -901,7 +902,7 @@ hipError_t gsr_depth_sort_compacted(const uint32_t *keys, int64_t n, uint32_t *b
                                     uint32_t *digit_total, uint32_t *ctl, int pass_begin,
                                     int pass_end, hipStream_t s, unsigned long long *host_D,
                                     uint32_t tag, uint32_t *ids_copy, hipEvent_t compacted,
-                                    const uint2 *keybits, int64_t n_keybits) {
+                                    int msd, const uint2 *keybits, int64_t n_keybits) {
     if (n <= 0 || pass_begin >= pass_end) return hipSuccess;
     if (n > (int64_t)UINT32_MAX || pass_begin < 0 || pass_end > kDPasses)
         return hipErrorInvalidValue;
@@ -916,7 +917,7 @@ hipError_t gsr_depth_sort_compacted(const uint32_t *keys, int64_t n, uint32_t *b
         }
     }
     // the passes read the compacted count from ctl[0] (grids sized for n)
-    if (keybits) {  // the MSD form, the whole sort at once (pass_begin 0 only)
+    if (msd) {  // the MSD form, the whole sort at once (pass_begin 0 only)
         if (pass_begin != 0) return hipErrorInvalidValue;
         // (pairs_b holds keys_c / ids_c: only the slow local sort of a degenerate bucket uses it,
         // after the MSD pass has read them)

@@ -265,8 +265,12 @@ bool gsr_color_ids_ok(const GsrPreprocessArgs &a);
 hipError_t gsr_launch_color_ids(const GsrPreprocessArgs &a, const uint32_t *ids,
                                 const uint32_t *d_n, int waves_per_simd, hipStream_t s);
 // K of the frame (sum of the preprocess blocks' pair counts), the pair count over the spans and
-// D -> a.host_K (pinned host memory), after the preprocess.
-hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s);
+// D -> a.host_K (pinned host memory), after the preprocess.  ds_ctl (optional): also the MSD
+// depth sort's control words, ctl[1] = D and ctl[2] = its pass's shift (gsr_depth_sort_msd
+// with keybits NULL), so the publish runs on the main stream in place of the sort's own
+// key-bit reduction.
+hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s,
+                                  uint32_t *ds_ctl = nullptr);
 hipError_t gsr_launch_mark_visible(const float *means3D, int64_t P, const float *viewmatrix,
                                    uint8_t *visible, hipStream_t s);
 hipError_t gsr_launch_view_depth_keys(const float *xyz, int64_t P, float v20, float v21, float v22,
@@ -321,7 +325,8 @@ hipError_t gsr_depth_sort(const uint32_t *keys, int64_t n, int drop, uint2 *pair
 // (keybits: n_keybits uint2, GsrPreprocessArgs.block_pairs after the counts), one global pass
 // over the top 12 of the D varying bits (dropping the 0xFFFFFFFF keys), then every bucket sorted
 // by the remaining bits in LDS.  Same result, ctl and perm contract as gsr_depth_sort with drop;
-// pairs_a holds the bucketed pairs, pairs_b is scratch.  host_D as in gsr_depth_sort.
+// pairs_a holds the bucketed pairs, pairs_b is scratch.  host_D as in gsr_depth_sort.  keybits
+// NULL: ctl[1] and ctl[2] are already set (gsr_launch_count_pairs with ds_ctl).
 hipError_t gsr_depth_sort_msd(const uint32_t *keys, int64_t n, const uint2 *keybits,
                               int64_t n_keybits, uint2 *pairs_a, uint2 *pairs_b, uint32_t *perm,
                               uint32_t *hist, uint32_t *digit_total, uint32_t *ctl, hipStream_t s,
@@ -330,9 +335,9 @@ hipError_t gsr_depth_sort_msd(const uint32_t *keys, int64_t n, const uint2 *keyb
 // (block_kept[b] of them, from the preprocess) are written in order to keys_c, their indices
 // to ids_c, and their count to ctl[0]; then the sort runs on those (gsr_depth_sort_compacted,
 // same contract as gsr_depth_sort with drop, n the uncompacted upper bound).  block_kept is
-// scanned in place.  keys_c / ids_c may be the two halves of pairs_b.  keybits (the preprocess
-// blocks' key OR / AND, as gsr_depth_sort_msd): the MSD form on the compacted keys instead of
-// the LSD passes (the whole sort in one call, pass_begin 0).
+// scanned in place.  keys_c / ids_c may be the two halves of pairs_b.  msd: the MSD form on the
+// compacted keys instead of the LSD passes (the whole sort in one call, pass_begin 0; keybits as
+// in gsr_depth_sort_msd).
 hipError_t gsr_depth_sort_compacted(const uint32_t *keys, int64_t n, uint32_t *block_kept,
                                     uint32_t *keys_c, uint32_t *ids_c, uint2 *pairs_a,
                                     uint2 *pairs_b, uint32_t *perm, uint32_t *hist,
@@ -340,7 +345,8 @@ hipError_t gsr_depth_sort_compacted(const uint32_t *keys, int64_t n, uint32_t *b
                                     int pass_end, hipStream_t s,
                                     unsigned long long *host_D = nullptr, uint32_t tag = 0,
                                     uint32_t *ids_copy = nullptr, hipEvent_t compacted = nullptr,
-                                    const uint2 *keybits = nullptr, int64_t n_keybits = 0);
+                                    int msd = 0, const uint2 *keybits = nullptr,
+                                    int64_t n_keybits = 0);
 
 // Binning: offsets scan over depth-sorted strip tile counts, duplicate into (tile, id)
 // pairs, and tile ranges.

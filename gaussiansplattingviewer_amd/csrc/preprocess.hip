@@ -509,7 +509,7 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
 __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__restrict__ cnt,
                                                     const uint2 *__restrict__ keybits, int64_t n,
                                                     unsigned long long *host_K,
-                                                    uint32_t k_tag) {
+                                                    uint32_t k_tag, uint32_t *ds_ctl) {
     __shared__ unsigned long long s_w[16], s_wt[16];
     __shared__ uint32_t s_or[16], s_and[16];
     unsigned long long v = 0, vt = 0;
@@ -560,6 +560,12 @@ __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__
         }
         const uint32_t diff = t ? (o ^ a) : 0u;
         const unsigned long long D = diff ? 32u - (uint32_t)__clz(diff) : 0u;
+        if (ds_ctl) {  // the MSD depth sort's D and shift (as k_ds_bits; OR == 0: no kept key)
+            const uint32_t kd = o ? (o ^ a) : 0u;
+            const uint32_t d2 = kd ? 32u - (uint32_t)__clz(kd) : 0u;
+            ds_ctl[1] = d2;
+            ds_ctl[2] = d2 > 12u ? d2 - 12u : 0u;
+        }
         __hip_atomic_store(host_K + 1, D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(host_K + 3, tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(host_K, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -739,13 +745,13 @@ hipError_t gsr_launch_color_ids(const GsrPreprocessArgs &a, const uint32_t *ids,
     return hipGetLastError();
 }
 
-hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s) {
+hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s, uint32_t *ds_ctl) {
     if (a.P == 0) return hipSuccess;
     const unsigned g = grid_for(a.P);  // the preprocess's blocks
     const uint2 *keybits = reinterpret_cast<const uint2 *>(a.block_pairs + g);
     hipLaunchKernelGGL(k_publish_K, dim3(1), dim3(1024), 0, s,
                        reinterpret_cast<const unsigned long long *>(a.block_pairs), keybits,
-                       (int64_t)g, a.host_K, a.k_tag);
+                       (int64_t)g, a.host_K, a.k_tag, ds_ctl);
     return hipGetLastError();
 }
 
