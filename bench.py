@@ -466,6 +466,11 @@ def main():
 
     # Frame statistics for the algorithmic byte counts (frame 0 of the camera path, full frame).
     res = scene.render(0, rows)
+    # the list entries that frame binned (tight binning: fewer than upstream's num_rendered)
+    K_list, T_all = ctypes.c_int64(), ctypes.c_int32()
+    _lib.check(_lib.load_library().gsr_get_binning(
+        _lib.context(local, 0), None, None, None, ctypes.byref(K_list), ctypes.byref(T_all),
+        ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "gsr_get_binning")
     P = scene.P
     P_v = int((res.radii > 0).sum().item())
     view = scene.cams[0][0]
@@ -517,7 +522,12 @@ def main():
                    "blend_arithmetic": args.blend},
         "msplats_per_sec": round(P * fps / 1e6, 2),
         "frame_stats": {"P_frustum": P_f, "P_visible": P_v, "K_pairs_mean": round(K_mean, 1),
-                        "tiles": T_strip},
+                        "K_list_frame0": int(K_list.value), "tiles": T_strip,
+                        "note": "K_pairs_mean is upstream's num_rendered (the SURVEY.md §8(d) "
+                                "bytes use it: an upper bound); K_list_frame0 the (Gaussian, "
+                                "tile) entries frame 0 binned and blended (tight binning on "
+                                "full frames keeps only tiles the alpha >= 1/255 ellipse "
+                                "reaches); msplats_per_sec counts Gaussians, not pairs"},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "stage_ms_note": "HIP events at every stage boundary, separate 30-frame serial pass "
                          "(each event adds a few us); the timed region records no events",
