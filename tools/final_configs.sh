@@ -25,6 +25,8 @@ for spec in ${CONFIGS:-c2 c3r c5 c4 c4:3/8 c3:3/8}; do
     python tools/sq_summary.py "$src" k_blend_q --json profiles/${T}_${key}_blend_sq.json \
         > gpurun_out/${T}_${key}_blend_sq.txt || exit 1
     cp profiles/${T}_${key}_kernels.json profiles/${T}_${key}_blend_sq.json gpurun_out/
+    # the raw traces stay on the box (gpurun copies back at most 64 MiB); the summaries travel
+    [ "${KEEP_RAW:-0}" = "1" ] || rm -rf "$src"
 done
 [ "${BENCH:-1}" = "1" ] && { bash tools/configs_bench.sh > gpurun_out/${T}_configs_bench.txt 2>&1 || exit 1; }
 exit 0
