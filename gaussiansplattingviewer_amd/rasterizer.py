@@ -179,6 +179,27 @@ def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales,
                                      rotations, cov3Ds_precomp, raster_settings)
 
 
+# upstream's debug dump (diff-gaussian-rasterization __init__.py; the reference ignores the file
+# in /root/reference/.gitignore:7)
+SNAPSHOT_FILE = "snapshot_fw.dump"
+
+
+def _cpu_copy(args):
+    """The `_C.rasterize_gaussians` argument tuple with every tensor copied to the host."""
+    return tuple(a.detach().cpu().clone() if isinstance(a, torch.Tensor) else a for a in args)
+
+
+def replay_snapshot(path: str = SNAPSHOT_FILE, device=None):
+    """Re-run a forward from a debug snapshot (the 19 `_C.rasterize_gaussians` arguments, tensors
+    on the host) on `device` (default: the current HIP device); returns upstream's 6-tuple.
+    Loaded with weights_only=True: the file holds tensors and plain numbers only."""
+    from . import _C
+    args = torch.load(path, weights_only=True)
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    args = tuple(a.to(dev) if isinstance(a, torch.Tensor) and a.numel() else a for a in args)
+    return _C.rasterize_gaussians(*args)
+
+
 class _RasterizeGaussians(torch.autograd.Function):
     """upstream `_RasterizeGaussians`: packs the settings into `_C.rasterize_gaussians`'s
     argument tuple and keeps (color, radii) of its 6-tuple.  Forward only (the viewer renders
@@ -196,10 +217,20 @@ class _RasterizeGaussians(torch.autograd.Function):
                 rs.scale_modifier, none(cov3Ds_precomp), rs.viewmatrix, rs.projmatrix,
                 rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, none(sh), rs.sh_degree,
                 rs.campos, rs.prefiltered, rs.debug)
-        if _lib._native_shares_library():
-            num_rendered, color, radii, geom, binning, img = _C.rasterize_gaussians(*args)
-        else:  # GSR_LIB (an A/B build): `_C` links the in-tree library, so render by ctypes
-            num_rendered, color, radii, _ = rasterize_gaussians_native(*args)
+        # debug (upstream __init__.py): the arguments are copied to the host first, and a
+        # forward that raises leaves them in SNAPSHOT_FILE for replay_snapshot()
+        cpu_args = _cpu_copy(args) if rs.debug else None
+        try:
+            if _lib._native_shares_library():
+                num_rendered, color, radii, geom, binning, img = _C.rasterize_gaussians(*args)
+            else:  # GSR_LIB (an A/B build): `_C` links the in-tree library, so render by ctypes
+                num_rendered, color, radii, _ = rasterize_gaussians_native(*args)
+        except Exception:
+            if cpu_args is not None:
+                torch.save(cpu_args, SNAPSHOT_FILE)
+                print(f"\nThe forward raised; its arguments are in {SNAPSHOT_FILE} "
+                      "(gaussiansplattingviewer_amd.rasterizer.replay_snapshot re-runs them).")
+            raise
         ctx.num_rendered = num_rendered
         ctx.mark_non_differentiable(radii)
         return color, radii

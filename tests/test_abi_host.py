@@ -107,6 +107,28 @@ def test_rasterizer_argument_checks_match_upstream():
           scales=torch.ones(4, 3), rotations=torch.ones(4, 4), cov3D_precomp=torch.ones(4, 6))
 
 
+def test_debug_forward_leaves_a_snapshot(tmp_path, monkeypatch):
+    """debug=True (upstream __init__.py): the arguments are copied to the host before the
+    forward, and a forward that raises writes them to snapshot_fw.dump in the working directory
+    (the file the reference ignores, /root/reference/.gitignore:7), then re-raises.  Without
+    debug nothing is written.  The dump loads with weights_only=True."""
+    from gaussiansplattingviewer_amd import rasterizer
+    monkeypatch.chdir(tmp_path)
+    x = torch.arange(16, dtype=torch.float32).reshape(4, 4)  # (P, 4): the extension refuses it
+    bad = dict(means3D=x, means2D=None, opacities=torch.ones(4, 1), shs=torch.ones(4, 1, 3),
+               scales=torch.ones(4, 3), rotations=torch.ones(4, 4))
+    with pytest.raises(RuntimeError, match=r"means3D must have dimensions \(num_points, 3\)"):
+        GaussianRasterizer(_settings())(**bad)
+    assert not (tmp_path / rasterizer.SNAPSHOT_FILE).exists()
+    with pytest.raises(RuntimeError, match=r"means3D must have dimensions \(num_points, 3\)"):
+        GaussianRasterizer(_settings()._replace(debug=True))(**bad)
+    args = torch.load(tmp_path / rasterizer.SNAPSHOT_FILE, weights_only=True)
+    assert len(args) == 19  # _C.rasterize_gaussians' arguments, in upstream's order
+    assert torch.equal(args[1], x) and args[1].device.type == "cpu"
+    assert args[12:14] == (64, 64) and args[15] == 0 and args[18] is True
+    assert args[2].numel() == 0 and torch.equal(args[14], torch.ones(4, 1, 3))  # colors absent
+
+
 def test_native_radii_optional_only_on_strips():
     with pytest.raises(RuntimeError, match="radii=False needs tile_rows"):
         rasterize_gaussians_native(torch.zeros(3), torch.zeros(4, 3), None, torch.ones(4, 1),

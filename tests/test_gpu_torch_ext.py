@@ -102,3 +102,18 @@ def test_rasterizer_module_and_mark_visible(gpu, oracle_mod):
     assert want.sum() > 0 and (~want).sum() > 0
     assert _C.mark_visible(torch.empty((0, 3), device=gpu), rs.viewmatrix,
                            rs.projmatrix).numel() == 0
+
+
+def test_debug_snapshot_replays(gpu, tmp_path):
+    """A debug snapshot (the 19 `_C.rasterize_gaussians` arguments on the host, as the debug
+    forward writes it when a forward raises) re-runs bit-identically through replay_snapshot."""
+    from gaussiansplattingviewer_amd import rasterizer
+    s = scene_inputs(synthetic_gaussians(30_000, 3, seed=5), static_camera(640, 480), 3)
+    args = _args(s, gpu)
+    want = _C.rasterize_gaussians(*args)
+    path = tmp_path / rasterizer.SNAPSHOT_FILE
+    torch.save(rasterizer._cpu_copy(args), path)
+    got = rasterizer.replay_snapshot(str(path), gpu)
+    assert got[0] == want[0]
+    torch.testing.assert_close(got[1], want[1], rtol=0, atol=0)
+    torch.testing.assert_close(got[2], want[2], rtol=0, atol=0)
