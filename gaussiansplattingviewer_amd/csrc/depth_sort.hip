@@ -678,13 +678,14 @@ __device__ void local_sort_big(uint2 *__restrict__ src, uint2 *__restrict__ tmp,
 // ballot per bit against a per-wave digit count in LDS (the lanes of a wave are in lockstep, so
 // no block barrier: the wavefront fences only keep the compiler from moving LDS accesses across
 // the hand-offs), scattered into the wave's LDS slice; the ids go to perm[b0 ...].
+template <int kIt>
 __device__ void wave_sort_bucket(const uint2 *__restrict__ src, uint32_t *__restrict__ perm,
                                  uint32_t b0, uint32_t n, int low, uint32_t *s_keys,
                                  uint32_t *s_vals, uint32_t *cnt) {
     const int lane = threadIdx.x & 63;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t lmask = (1u << low) - 1u;
-    constexpr int kIt = kLWave / 64;
+    static_assert(kIt * 64 <= kLWave, "the wave's LDS slice");
     uint32_t k[kIt], v[kIt];
 #pragma unroll
     for (int j = 0; j < kIt; ++j) {
@@ -796,9 +797,13 @@ __global__ __launch_bounds__(kDThreads) void k_ds_local(uint2 *__restrict__ pair
     }
     {
         const uint32_t b0 = sm.start[w], bn = sm.start[w + 1] - b0;
-        if (bn > 0u && bn <= (uint32_t)kLWave)
-            wave_sort_bucket(pairs, perm, b0, bn, low, sm.keys + w * kLWave, sm.vals + w * kLWave,
-                             sm.wcnt + w * kDSubBins);
+        // (a bucket of <= 256 keys takes 4 per lane: half the ranking work of 8)
+        if (bn > 0u && bn <= (uint32_t)kLWave / 2)
+            wave_sort_bucket<kLWave / 128>(pairs, perm, b0, bn, low, sm.keys + w * kLWave,
+                                           sm.vals + w * kLWave, sm.wcnt + w * kDSubBins);
+        else if (bn > 0u && bn <= (uint32_t)kLWave)
+            wave_sort_bucket<kLWave / 64>(pairs, perm, b0, bn, low, sm.keys + w * kLWave,
+                                          sm.vals + w * kLWave, sm.wcnt + w * kDSubBins);
     }
     __syncthreads();
     for (int i = 0; i < kLGroup; ++i) {  // the larger buckets, one at a time by the block
