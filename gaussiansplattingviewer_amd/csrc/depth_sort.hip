@@ -797,13 +797,17 @@ __global__ __launch_bounds__(kDThreads) void k_ds_local(uint2 *__restrict__ pair
     }
     {
         const uint32_t b0 = sm.start[w], bn = sm.start[w + 1] - b0;
-        // (a bucket of <= 256 keys takes 4 per lane: half the ranking work of 8)
-        if (bn > 0u && bn <= (uint32_t)kLWave / 2)
-            wave_sort_bucket<kLWave / 128>(pairs, perm, b0, bn, low, sm.keys + w * kLWave,
-                                           sm.vals + w * kLWave, sm.wcnt + w * kDSubBins);
-        else if (bn > 0u && bn <= (uint32_t)kLWave)
-            wave_sort_bucket<kLWave / 64>(pairs, perm, b0, bn, low, sm.keys + w * kLWave,
-                                          sm.vals + w * kLWave, sm.wcnt + w * kDSubBins);
+        // keys per lane by the bucket's size (the ranking work is per item): 2, 4 or 8
+        uint32_t *sk = sm.keys + w * kLWave, *sv = sm.vals + w * kLWave;
+        uint32_t *sc = sm.wcnt + w * kDSubBins;
+        if (bn == 0u) {
+        } else if (bn <= 128u) {
+            wave_sort_bucket<2>(pairs, perm, b0, bn, low, sk, sv, sc);
+        } else if (bn <= 256u) {
+            wave_sort_bucket<4>(pairs, perm, b0, bn, low, sk, sv, sc);
+        } else if (bn <= (uint32_t)kLWave) {
+            wave_sort_bucket<kLWave / 64>(pairs, perm, b0, bn, low, sk, sv, sc);
+        }
     }
     __syncthreads();
     for (int i = 0; i < kLGroup; ++i) {  // the larger buckets, one at a time by the block
