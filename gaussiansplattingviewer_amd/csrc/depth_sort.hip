@@ -16,6 +16,8 @@
 //     needed pass writes the permutation straight to `perm`;
 //   * compaction: pass 0 drops the sentinel keys (0xFFFFFFFF: Gaussians without pairs in the
 //     strip) and stores the kept count on the device; later passes read it.
+// The frame's default form (gsr_depth_sort_msd, below) replaces the LSD passes by one MSD pass
+// over the top 12 of the D bits and an in-LDS sort of every bucket by the rest.
 // Each pass is three kernels: upsweep (per-tile 4096-bin histogram, LDS atomics), scan (per
 // digit across tiles) and downsweep.  Between passes the (key, id) pairs travel as one 8-B
 // word each.  The downsweep sorts its 4096-key tile in LDS by
