@@ -432,3 +432,39 @@ def test_compacted_strip_colour_path(gpu, form):
                 np.testing.assert_array_equal(lean[k], part[k], err_msg=k)
     finally:
         _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, -1)
+
+
+def test_msd_local_sort_tier_boundaries(gpu, oracle_mod):
+    """k_ds_local sorts a bucket with 2, 4 or 8 keys per lane by its size (<= 128, <= 256,
+    <= 512 keys; larger ones by the whole block): buckets of the MSD pass's top 12 key bits are
+    built with sizes on both sides of every boundary (depths 2..8: D = 24, bucket = key bits
+    12..23), then the frame must match the oracle."""
+    rng = np.random.default_rng(41)
+    sizes = [1, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512, 513, 700, 2000]
+    keys = [np.uint32(0x40000000 | (4095 << 12) | 2048)]  # the deepest key: bit 23 set, D = 24
+    for i, n in enumerate(sizes):
+        b = 16 + 211 * i  # well-separated buckets below 4095
+        low = rng.integers(256, 3840, n).astype(np.uint32)  # away from the bucket's edges
+        keys.append(np.uint32(0x40000000) | np.uint32(b << 12) | low)
+    keys = np.concatenate([np.atleast_1d(k) for k in keys]).astype(np.uint32)
+    P = len(keys)
+    g = synthetic_gaussians(P, 3, 41)
+    g.xyz[:, :2] = rng.uniform(-0.15, 0.15, (P, 2)).astype(np.float32)
+    g.xyz[:, 2] = np.float32(3.0) - keys.view(np.float32)  # view depth 3 - z from (0, 0, 3)
+    g.scale[:] = np.float32(0.005)
+    g.opacity[:] = np.float32(3.0)
+    s = scene_inputs(g, static_camera(320, 240, (0, 0, 3.0)), 3)
+    orc = run_oracle(oracle_mod, s)
+    d = orc["depths"][orc["radii"] > 0].view(np.uint32)
+    D = int(np.bitwise_or.reduce(d) ^ np.bitwise_and.reduce(d)).bit_length()
+    counts = np.bincount((d >> np.uint32(D - 12)) & np.uint32(4095), minlength=4096)
+    assert D == 24, D
+    for edge in (128, 256, 512):  # sizes on both sides of every tier boundary
+        assert ((counts > 0) & (counts <= edge) & (counts > edge - 3)).any(), (edge, counts[counts > 0])
+        assert ((counts > edge) & (counts < edge + 3)).any(), (edge, counts[counts > 0])
+    _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, 2)
+    try:
+        hip = run_hip(s, gpu)
+    finally:
+        _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, -1)
+    assert_parity(hip, orc)
