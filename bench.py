@@ -50,6 +50,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 
 CONFIGS = {
     # name: (P, W, H, sh_degree, seed, camera[, scene generator])
+    # BASELINE.json configs[0]: the reference's CPU path (numpy sort, renderer_ogl.py:10-19) and
+    # the CPU restatement of the blend at 10k / 640x480, timed by cpu_baseline; the HIP forward
+    # of the same frame beside it
+    "c1": (10_000, 640, 480, 3, 0, "static"),
     "c2": (100_000, 1920, 1080, 0, 1, "static"),
     "c3": (1_000_000, 1920, 1080, 3, 2, "static"),
     "c4": (6_000_000, 3840, 2160, 3, 3, "static"),
@@ -239,6 +243,32 @@ def algorithmic_bytes(P, P_f, P_v, K, T, W, H, sh_bytes):
         "tile_sort": 24 * K,    # one read + write of 12-B pairs (upstream's pair size)
         "ranges": 8 * K + 8 * T,
         "blend": 40 * K + 12 * W * H,
+    }
+
+
+def design_bytes(P, P_f, P_v, K_L, T, W, H, sh_bytes):
+    """This design's minimum HBM bytes per frame: what each of its kernels must
+    read and write once, with the pair list it really bins (K_L 4-B list words after tight
+    binning) -- beside SURVEY.md §8(d)'s upstream model, which charges 12-B pairs for upstream's
+    K and a 24-B-per-pair sort that this design does not do."""
+    return {
+        # xyz; scale + rotation + opacity in the frustum; depth key, {rect, span} record, the
+        # blend's 36-B record of a visible Gaussian
+        "preprocess": 12 * P + 32 * P_f + 4 * P + 16 * P + 36 * P_v,
+        # the rect flag, the SH row and the 12-B colour of a visible Gaussian
+        "color": 8 * P + (sh_bytes + 12) * P_v,
+        # keys in, (key, id) pairs out and back in, the permutation out
+        "depth_sort": 4 * P + 20 * P_v,
+        # the permutation and the gathered + written 16-B records
+        "scan": 36 * P_v,
+        # the permutation and the records in depth order, the list words out
+        "duplicate": 20 * P_v + 4 * K_L,
+        # the row pass: upsweep read, downsweep read + write
+        "tile_sort": 12 * K_L,
+        # the second stream's tile counts over the records, the ranges out
+        "ranges": 16 * P + 8 * T,
+        # a list word and a 48-B record per list entry, the image out
+        "blend": 52 * K_L + 12 * W * H,
     }
 
 
@@ -497,6 +527,18 @@ def main():
     roofline = blend_roofline(prof_key if default_opts else None, dom_ms, blend_ms_timed,
                               alg["blend"])
     roofline["frame_alg_gbs"] = round(sum(alg.values()) / (t_max / args.steps) / 1e9, 2)
+    # the design's own minimum bytes (frame 0's list length) over the same frame time
+    dsg = design_bytes(P, P_f, P_v, int(K_list.value), T_strip, W, rows_px, sh_bytes)
+    dsg_gbs = sum(dsg.values()) / (t_max / args.steps) / 1e9
+    roofline["frame_design"] = {
+        "bytes_per_frame": int(sum(dsg.values())), "gbs": round(dsg_gbs, 2),
+        "frac_of_hbm": round(dsg_gbs / HBM_PEAK_GBS, 4),
+        "per_stage_bytes": {k: int(v) for k, v in dsg.items()},
+        "note": "this design's minimum HBM bytes per frame (bench.design_bytes: the 4-B list "
+                "words it bins, one read + write of the depth sort's 8-B pairs, the 48-B blend "
+                "records per list entry) over the timed frame time; frame_alg_gbs above is "
+                "SURVEY.md 8(d)'s upstream model (12-B pairs, upstream's K), which can exceed "
+                "the peak on this design"}
     fps = args.steps / t_max
     line = {
         "metric": METRIC,
@@ -539,6 +581,7 @@ def main():
                           "rebalances": len(balancer.history),
                           "note": "cost-weighted strips (StripBalancer): every 8 frames the "
                                   "ranks all-reduce their tile rows' pair counts and re-split"}),
+        "frame_graphs": {f"slot{c}": _lib.frame_graph_stats(local, c) for c in range(args.inflight)},
         "serial_ms_per_frame": round(serial_ms, 4),
         "serial_note": "one frame in flight at a time (no FramePipeline overlap), this rank",
         "roofline": roofline,

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import atexit
 import ctypes
+import functools
 import os
 import threading
 
@@ -19,6 +20,7 @@ GSR_OPT_BLEND_CULL = 1
 GSR_OPT_BLEND_FAST = 2
 GSR_OPT_DEPTH_SORT = 11
 GSR_OPT_TIGHT_BINNING = 13
+GSR_OPT_FRAME_GRAPHS = 14
 
 # Symbols include/gsr.h declares (checked by the CPU test suite).
 EXPORTED_SYMBOLS = (
@@ -26,7 +28,7 @@ EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_get_binning", "gsr_mark_visible", "gsr_depth_argsort",
     "gsr_set_timing", "gsr_stage_times", "gsr_stage_name", "gsr_set_option",
     "gsr_ply_probe", "gsr_ply_load", "gsr_disparity_colors", "gsr_pack_image",
-    "gsr_tile_row_pairs",
+    "gsr_tile_row_pairs", "gsr_frame_graph_stats",
 )
 
 GSR_PACK_RGBA_F32 = 0
@@ -99,6 +101,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.gsr_stage_name.argtypes = [i32]
     lib.gsr_stage_name.restype = ctypes.c_char_p
     lib.gsr_set_option.argtypes = [vp, i32, i64]
+    lib.gsr_frame_graph_stats.argtypes = [vp, ctypes.POINTER(i64), i32]
     lib.gsr_ply_probe.argtypes = [ctypes.c_char_p, ctypes.POINTER(GsrPlyInfo)]
     lib.gsr_ply_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(GsrPlyInfo), vp, vp, vp, vp, vp,
                                  i32, vp]
@@ -108,7 +111,8 @@ def _declare(lib: ctypes.CDLL) -> None:
                                    ctypes.c_int32, vp, vp]
     for name in ("gsr_disparity_colors", "gsr_pack_image", "gsr_create", "gsr_reserve", "gsr_forward", "gsr_get_binning",
                  "gsr_mark_visible", "gsr_depth_argsort", "gsr_set_timing", "gsr_tile_row_pairs",
-                 "gsr_stage_times", "gsr_set_option", "gsr_ply_probe", "gsr_ply_load"):
+                 "gsr_stage_times", "gsr_set_option", "gsr_ply_probe", "gsr_ply_load",
+                 "gsr_frame_graph_stats"):
         getattr(lib, name).restype = i32
 
 
@@ -139,9 +143,11 @@ def check(rc: int, what: str) -> int:
     return rc
 
 
+@functools.lru_cache(maxsize=None)
 def _native_shares_library() -> bool:
     """The `_native` extension links the in-tree libgsr.so; contexts are shared with it only
-    when this module loaded that same file (not a GSR_LIB A/B build)."""
+    when this module loaded that same file (not a GSR_LIB A/B build).  LIB_PATH is fixed at
+    import, so the answer is computed once (the forward asks on every frame)."""
     default = os.path.join(_HERE, "libgsr.so")
     return (os.path.exists(LIB_PATH) and os.path.exists(default) and
             os.path.samefile(LIB_PATH, default))
@@ -197,6 +203,14 @@ def release_contexts() -> None:
 
 
 atexit.register(release_contexts)
+
+
+def frame_graph_stats(device_index: int = 0, slot: int = 0) -> dict:
+    """Frame-graph counters of a context slot (gsr_frame_graph_stats)."""
+    lib = load_library()
+    v = (ctypes.c_int64 * 4)()
+    check(lib.gsr_frame_graph_stats(context(device_index, slot), v, 4), "gsr_frame_graph_stats")
+    return {"graph_frames": v[0], "graphs_recorded": v[1], "overflows": v[2], "list_cap": v[3]}
 
 
 def stage_names() -> list[str]:

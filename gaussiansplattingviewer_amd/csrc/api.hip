@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "gsr.h"
 #include "gsr_internal.h"
@@ -78,6 +79,33 @@ constexpr uint32_t kMsdMaxD = 24;
 const char *kStageNames[kAllStages] = {"preprocess", "depth_sort", "scan",  "duplicate",
                                        "tile_sort",  "ranges",     "blend", "color"};
 
+// Frame graphs: recorded pairs of graphs kept per context (least recently used replaced), and
+// executable graphs replaced while possibly in flight, kept until a synchronisation point.
+constexpr size_t kGraphCache = 4;
+constexpr size_t kGraphRetired = 16;
+// The binning capacity of frame graphs: the list length seen so far plus a quarter, at least
+// kMinListCap entries.
+constexpr int64_t kMinListCap = 1 << 16;
+
+// Everything the kernels of a frame's recorded graphs read besides the context's own
+// workspace (named by its generation): a forward whose key equals a recorded one replays it.
+struct GraphKey {
+    uint64_t ws_gen;
+    int64_t cap, P;
+    const void *means3D, *shs, *colors_precomp;
+    int32_t D, M, W, H;
+    uint32_t gx, gy, rb, re;
+    int32_t col_shift, color_waves;
+    uint8_t msd, main_publish, tight, sh_vec4;
+};
+
+struct GraphEntry {
+    GraphKey key;
+    hipGraphExec_t main = nullptr, aux = nullptr;  // the frame stream's and the second stream's
+    uint32_t *point_list = nullptr;                // the list the recorded row pass leaves
+    uint64_t used = 0;                             // LRU stamp
+};
+
 }  // namespace
 
 struct gsr_context {
@@ -104,7 +132,9 @@ struct gsr_context {
     unsigned long long *d_hostK = nullptr;  // device view of h_total + 2
     unsigned long long *d_hostD = nullptr;  // device view of h_total + 4
     uint32_t sort_tag = 0;                  // frames rendered on this context (the pinned tags)
-    uint32_t last_D = 0;                    // key bits of the last frame's kept depths
+    // key bits of the last frame's kept depths (wait_K); the first frame, with no history,
+    // takes the LSD sort, which any spread of depths suits (the MSD form wants D <= 24)
+    uint32_t last_D = UINT32_MAX;
     // state of the last forward (gsr_get_binning, gsr_tile_row_pairs)
     bool have_forward = false;
     int64_t last_K = 0;        // upstream's num_rendered
@@ -130,6 +160,19 @@ struct gsr_context {
     hipStream_t aux = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
     hipEvent_t compacted = nullptr;  // the compacted ids are written (main -> second stream)
+    // frame graphs (GSR_OPT_FRAME_GRAPHS, DESIGN.md decision 12): the frame stream's chain after
+    // the preprocess and the second stream's chain, each recorded once as a linear graph and
+    // replayed while the key matches; the binning is sized by a capacity instead of the host
+    // waiting for K in mid-frame
+    int graphs = 0;
+    DevBuf frame_words;                  // [0] tag, [1] list length, [4..6] campos
+    uint32_t ws_gen = 0;                 // bumped by every (re)allocation of a workspace buffer
+    int64_t list_cap = 0;                // pair-list capacity of the graphs (0: none yet)
+    hipStream_t cap_stream = nullptr;    // private stream the graphs are recorded on
+    std::vector<GraphEntry> graph_cache;
+    std::vector<hipGraphExec_t> graph_retired;
+    uint64_t graph_clock = 0;
+    int64_t graph_frames = 0, graph_records = 0, graph_overflows = 0;  // (gsr_graph_stats)
 };
 
 namespace {
@@ -147,6 +190,7 @@ int grow(gsr_context *ctx, DevBuf &b, size_t bytes, hipStream_t s) {
         b.p = nullptr;
         b.cap = 0;
     }
+    ++ctx->ws_gen;  // recorded frame graphs hold the old pointers
     if (hipMalloc(&b.p, want) != hipSuccess) {
         (void)hipGetLastError();
         b.p = nullptr;
@@ -167,7 +211,7 @@ int reserve_P(gsr_context *ctx, int64_t P, hipStream_t s) {
     GSR_TRY(grow(ctx, ctx->partials, (size_t)std::max<int64_t>(gsr_scan_blocks(P), 1) * 4, s));
     GSR_TRY(grow(ctx, ctx->total, 16, s));
     // per preprocess block: its pair count (8 B) and kept-key OR / AND (8 B)
-    GSR_TRY(grow(ctx, ctx->pair_count, (size_t)std::max<int64_t>((P + 255) / 256, 1) * 16, s));
+    GSR_TRY(grow(ctx, ctx->pair_count, (size_t)std::max<int64_t>(gsr_preprocess_blocks(P), 1) * 16, s));
     GSR_TRY(grow(ctx, ctx->hist, (size_t)std::max(gsr_radix_hist_words(P),
                                                   gsr_depth_sort_hist_words(P)) * 4, s));
     // column-first binning's per-(block, column) counts: its own buffer, since reserve_K may
@@ -233,6 +277,7 @@ struct Frame {
                         // second
     bool color_ids;     // the colour pass walks the compacted ids
     bool colpairs;      // column-first binning (else the per-pair form)
+    bool graph = false;  // this forward replays recorded frame graphs (forward_graph)
     int col_shift;      // column pairs: packed word = strip row << col_shift | Gaussian id
     uint32_t tag;       // this frame's tag for the pinned words
     GsrPreprocessArgs pa;
@@ -414,7 +459,7 @@ int launch_depth_sort(gsr_context *ctx, const Frame &f, int p0, int p1) {
     uint32_t *perm = static_cast<uint32_t *>(ctx->perm.p);
     uint2 *ds_a = static_cast<uint2 *>(ctx->ds_a.p), *ds_b = static_cast<uint2 *>(ctx->ds_b.p);
     hipError_t e;
-    const int64_t nb = (f.P + 255) / 256;  // preprocess blocks (their key OR / AND words)
+    const int64_t nb = gsr_preprocess_blocks(f.P);  // (their key OR / AND words)
     const uint2 *keybits = reinterpret_cast<const uint2 *>(f.pa.block_pairs + nb);
     if (f.compact_sort) {
         // the compacted keys / ids live in ds_b until pass 1 (or the MSD pass) has read them
@@ -431,24 +476,31 @@ int launch_depth_sort(gsr_context *ctx, const Frame &f, int p0, int p1) {
         // MSD pass + per-bucket local sort, the whole sort at once (D from the preprocess blocks)
         if (p0 != 0) return GSR_OK;  // (no later passes)
         e = gsr_depth_sort_msd(f.pa.sort_keys, f.P, f.main_publish ? nullptr : keybits, nb,
-                               ds_a, ds_b, perm, hist, digit_total, ctl, f.s, ctx->d_hostD,
-                               f.tag);
-    } else {
+                               ds_a, ds_b, perm, hist, digit_total, ctl, f.s,
+                               f.graph ? nullptr : ctx->d_hostD, f.tag);
+    } else {  // (frame graphs queue every pass; the host reads no D)
         e = gsr_depth_sort(f.pa.sort_keys, f.P, 1, ds_a, ds_b, perm, hist, digit_total, ctl, p0,
-                           p1, f.s, ctx->d_hostD, f.tag);
+                           p1, f.s, f.graph ? nullptr : ctx->d_hostD, f.tag);
     }
     GSR_HIP(e, "depth sort launch");
     return GSR_OK;
 }
 
+// colour waves per SIMD (gsr_launch_color): 2 on a full frame, so the colour leaves the CUs
+// to the binning chain it overlaps (C3 two frames in flight 3,890-3,918 -> 3,947-3,954
+// frames/s, serial 0.317 -> 0.308 ms; C4 serial 2.09 -> 2.06 ms); 3 on a compacted strip
+// (C4 1/8 strip 0.481 -> 0.468 ms).  profiles/r04n_ab_color_waves.txt, DESIGN.md decision 7
+int color_waves_of(const Frame &f) { return f.color_ids ? 3 : 2; }
+
 // ---- the second stream: K, the tile ranges (column pairs), the colour -----------------------
-int launch_second_stream(gsr_context *ctx, const Frame &f) {
-    hipStream_t as = ctx->aux;
-    GSR_HIP(hipStreamWaitEvent(as, ctx->fork, 0), "hipStreamWaitEvent(fork)");
+// The second stream's kernels on stream `as` (a frame graph records them on its capture
+// stream; d_tag then names the device word holding the frame's tag).
+int aux_chain(gsr_context *ctx, const Frame &f, hipStream_t as, const uint32_t *d_tag) {
     // K first: k_publish_K sums the preprocess blocks' counts into pinned memory; the host
     // waits for it only after the depth sort and the column counts are queued (MSD frames
     // publish on the main stream instead, with the sort's D)
-    if (!f.main_publish) GSR_HIP(gsr_launch_count_pairs(f.pa, as), "pair count launch");
+    if (!f.main_publish)
+        GSR_HIP(gsr_launch_count_pairs(f.pa, as, nullptr, d_tag), "pair count launch");
     if (f.tmode == 1) GSR_HIP(hipEventRecord(f.evc[0], as), "hipEventRecord");
     // the tile ranges before the colour, so the colour overlaps the column count and scatter
     // rather than the depth sort (C3 two frames in flight 3,470 -> 3,600 frames/s)
@@ -464,11 +516,7 @@ int launch_second_stream(gsr_context *ctx, const Frame &f) {
                                        static_cast<uint32_t *>(ctx->blend_order.p), as),
                 "blend order launch");
     }
-    // colour waves per SIMD (gsr_launch_color): 2 on a full frame, so the colour leaves the CUs
-    // to the binning chain it overlaps (C3 two frames in flight 3,890-3,918 -> 3,947-3,954
-    // frames/s, serial 0.317 -> 0.308 ms; C4 serial 2.09 -> 2.06 ms); 3 on a compacted strip
-    // (C4 1/8 strip 0.481 -> 0.468 ms).  profiles/r04n_ab_color_waves.txt, DESIGN.md decision 7
-    const int color_waves = f.color_ids ? 3 : 2;
+    const int color_waves = color_waves_of(f);
     if (f.color_ids) {
         GSR_HIP(hipStreamWaitEvent(as, ctx->compacted, 0), "hipStreamWaitEvent(compacted)");
         GSR_HIP(gsr_launch_color_ids(f.pa, static_cast<const uint32_t *>(ctx->color_ids.p),
@@ -479,6 +527,13 @@ int launch_second_stream(gsr_context *ctx, const Frame &f) {
         GSR_HIP(gsr_launch_color(f.pa, color_waves, as), "color launch");
     }
     if (f.tmode == 1) GSR_HIP(hipEventRecord(f.evc[1], as), "hipEventRecord");
+    return GSR_OK;
+}
+
+int launch_second_stream(gsr_context *ctx, const Frame &f) {
+    hipStream_t as = ctx->aux;
+    GSR_HIP(hipStreamWaitEvent(as, ctx->fork, 0), "hipStreamWaitEvent(fork)");
+    GSR_TRY(aux_chain(ctx, f, as, nullptr));
     GSR_HIP(hipEventRecord(ctx->join, as), "hipEventRecord(join)");
     if (f.dbg) GSR_HIP(hipStreamSynchronize(as), "stage color");
     return GSR_OK;
@@ -508,6 +563,14 @@ int launch_scan(gsr_context *ctx, const Frame &f) {
                 "scan launch");
     }
     return GSR_OK;
+}
+
+// The frame graphs' list capacity for a list of n entries (capacity cap so far): a quarter more,
+// at least kMinListCap, 4096-aligned (the row pass's tiles), and at least 1.5x the old one.
+int64_t list_capacity(int64_t n, int64_t cap) {
+    int64_t c = std::max({n + n / 4, kMinListCap, cap + cap / 2});
+    c = (c + 4095) & ~(int64_t)4095;
+    return std::min<int64_t>(c, (int64_t)UINT32_MAX - 4096);
 }
 
 // K (the pair count, which sizes the binning) from k_publish_K on the second stream, published
@@ -541,7 +604,14 @@ int wait_K(gsr_context *ctx, Frame &f) {
     }
     if (f.K > (uint64_t)UINT32_MAX - 4096)
         return fail(GSR_E_INVALID, "gsr_forward: more than 2^32-4097 (Gaussian, tile) pairs");
-    return reserve_K(ctx, (int64_t)f.KL, f.s);
+    // column-first frames also size the frame graphs' list capacity (before the binning, so
+    // this frame's list is not reallocated under it)
+    int64_t want = (int64_t)f.KL;
+    if (ctx->graphs && f.colpairs && want > ctx->list_cap) {
+        ctx->list_cap = list_capacity(want, ctx->list_cap);
+        want = ctx->list_cap;
+    }
+    return reserve_K(ctx, want, f.s);
 }
 
 // ---- 4 + 5. the pairs, stably sorted by strip tile ------------------------------------------
@@ -639,6 +709,10 @@ int launch_blend(gsr_context *ctx, const Frame &f, const gsr_raster_settings *st
     ba.id_mask = f.id_mask;
     ba.order = f.colpairs ? static_cast<const uint32_t *>(ctx->blend_order.p)
                           : nullptr;  // (per-pair form: row-major)
+    if (f.graph) {  // the list length is on the device: a list over the capacity is not blended
+        ba.list_n = static_cast<const uint32_t *>(ctx->frame_words.p) + 1;
+        ba.list_cap = (uint32_t)ctx->list_cap;
+    }
     GSR_HIP(gsr_launch_blend(ba, f.s), "blend launch");
     return GSR_OK;
 }
@@ -654,11 +728,258 @@ struct JoinGuard {
     }
 };
 
+// The state gsr_get_binning / gsr_tile_row_pairs read, after a rendered frame.
+void finish_frame(gsr_context *ctx, const Frame &f, gsr_outputs *out) {
+    out->num_rendered = (int64_t)f.K;
+    ctx->last_K = (int64_t)f.K;
+    ctx->last_list = (int64_t)f.KL;
+    ctx->last_tight = f.tight;
+    ctx->last_gx = f.gx, ctx->last_gy = f.gy, ctx->last_rb = f.rb, ctx->last_re = f.re;
+    ctx->last_point_list = f.point_list;
+    ctx->last_tiles_local = f.tiles_local;
+    ctx->last_id_mask = f.id_mask;
+    ctx->last_packed = f.colpairs && f.KL > 0;
+    ctx->have_forward = true;
+    if (f.tmode) ++ctx->timed_frames;
+}
+
+// ---- frame graphs (DESIGN.md decision 12) -----------------------------------------------------
+// A small frame is bound by the host: ~17 kernel launches at ~5 us each.  ROCm launches a linear
+// graph as one batch of pre-built packets (a 20-kernel chain in ~6 us), so the frame stream's
+// chain after the preprocess (K publish, depth sort, column counts, column scatter, row pass)
+// and the second stream's chain (tile ranges, blend order, colour) are each recorded once as a
+// linear graph and replayed; the preprocess (the frame's camera and outputs) and the blend (its
+// image) stay direct launches, so 2 launches + 2 graph launches + the fork / join remain.  A
+// graph cannot take per-frame arguments: the preprocess stores the frame's tag and camera
+// position into device words the recorded kernels read, and the binning is sized by a capacity
+// (the list lengths seen so far + 25 %) instead of the host waiting for K in mid-frame; the
+// column scatter stores the true length on the device and the row pass and the blend do
+// nothing when it exceeds the capacity.  The host reads K after queueing the whole frame (for
+// num_rendered) and re-renders an overflowed frame the direct way with a larger capacity, so
+// every returned image is complete.
+
+// Eligible forwards: column-first binning, a known capacity, no debug, no per-stage timing, no
+// compaction (its colour pass waits on a mid-chain event of the frame stream), no rgb output
+// (the colour pass's).
+bool graph_eligible(const gsr_context *ctx, const Frame &f, const gsr_outputs *out) {
+    return ctx->graphs && ctx->list_cap > 0 && f.colpairs && !f.dbg && f.tmode != 1 &&
+           !f.compact_sort && !f.color_ids && !out->rgb && f.P > 0;
+}
+
+GraphKey graph_key(const gsr_context *ctx, const Frame &f) {
+    GraphKey k;
+    std::memset(&k, 0, sizeof(k));  // (padding compares equal)
+    k.ws_gen = ctx->ws_gen;
+    k.cap = ctx->list_cap;
+    k.P = f.P;
+    k.means3D = f.pa.means3D;
+    k.shs = f.pa.shs;
+    k.colors_precomp = f.pa.colors_precomp;
+    k.D = f.pa.D;
+    k.M = f.pa.M;
+    k.W = f.W;
+    k.H = f.H;
+    k.gx = f.gx;
+    k.gy = f.gy;
+    k.rb = f.rb;
+    k.re = f.re;
+    k.col_shift = f.col_shift;
+    k.color_waves = color_waves_of(f);
+    k.msd = f.msd_sort;
+    k.main_publish = f.main_publish;
+    k.tight = f.tight;
+    k.sh_vec4 = (uint8_t)f.pa.sh_vec4;
+    return k;
+}
+
+// The preprocess arguments the recorded kernels see: the camera position from the frame
+// words, and none of the per-frame pointers (camera matrices, outputs), which they do not read.
+GsrPreprocessArgs graph_args(const gsr_context *ctx, const GsrPreprocessArgs &a) {
+    GsrPreprocessArgs g = a;
+    uint32_t *fw = static_cast<uint32_t *>(ctx->frame_words.p);
+    g.campos = a.campos ? reinterpret_cast<const float *>(fw + 4) : nullptr;
+    g.viewmatrix = g.projmatrix = nullptr;
+    g.scales = g.rotations = g.opacities = g.cov3D_precomp = nullptr;
+    g.radii = nullptr;
+    g.depths = g.means2D = g.conic_opacity = g.rgb = nullptr;
+    g.tiles_touched = nullptr;
+    g.k_tag = 0;
+    g.frame_words = nullptr;
+    return g;
+}
+
+void retire_graph(gsr_context *ctx, GraphEntry &e) {
+    if (e.main) ctx->graph_retired.push_back(e.main);
+    if (e.aux) ctx->graph_retired.push_back(e.aux);
+    e.main = e.aux = nullptr;
+}
+
+// Destroys the retired executable graphs once enough have gathered (they ran only on this
+// context's frame stream and second stream, which are drained first).
+int drain_retired(gsr_context *ctx, hipStream_t s, bool force) {
+    if (ctx->graph_retired.empty() || (!force && ctx->graph_retired.size() < kGraphRetired))
+        return GSR_OK;
+    GSR_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(graphs)");
+    GSR_HIP(hipStreamSynchronize(ctx->aux), "hipStreamSynchronize(graphs)");
+    for (hipGraphExec_t ge : ctx->graph_retired) (void)hipGraphExecDestroy(ge);
+    ctx->graph_retired.clear();
+    return GSR_OK;
+}
+
+// Records one chain on the context's capture stream into an executable graph.
+template <typename Chain>
+int record_chain(gsr_context *ctx, Chain chain, hipGraphExec_t *out) {
+    hipStream_t cs = ctx->cap_stream;
+    GSR_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+    const int rc = chain(cs);
+    hipGraph_t graph = nullptr;
+    const hipError_t e = hipStreamEndCapture(cs, &graph);  // (ends the capture on every path)
+    if (rc != GSR_OK) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return rc;
+    }
+    GSR_HIP(e, "hipStreamEndCapture");
+    const hipError_t ei = hipGraphInstantiate(out, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    GSR_HIP(ei, "hipGraphInstantiate");
+    return GSR_OK;
+}
+
+// Records the frame's two chains (the key's) into e.
+int record_frame_graphs(gsr_context *ctx, const Frame &f, GraphEntry &e) {
+    Frame g = f;
+    g.pa = graph_args(ctx, f.pa);
+    g.tmode = 0;
+    const uint32_t *fw = static_cast<const uint32_t *>(ctx->frame_words.p);
+    uint32_t *list_n = static_cast<uint32_t *>(ctx->frame_words.p) + 1;
+    GSR_TRY(record_chain(ctx, [&](hipStream_t cs) -> int {
+        g.s = cs;
+        if (g.main_publish)
+            GSR_HIP(gsr_launch_count_pairs(g.pa, cs, static_cast<uint32_t *>(ctx->ds_ctl.p), fw),
+                    "pair count launch");
+        GSR_TRY(launch_depth_sort(ctx, g, 0, gsr_depth_sort_passes(32)));
+        GSR_TRY(launch_scan(ctx, g));
+        // the column scatter and the row pass over the capacity, the length read on the device
+        const int64_t cap = ctx->list_cap;
+        uint32_t *tv = static_cast<uint32_t *>(ctx->tile_vals.p);
+        uint32_t *tv_alt = static_cast<uint32_t *>(ctx->tile_vals_alt.p);
+        GSR_HIP(gsr_launch_col_pairs_scatter(
+                    static_cast<const uint32_t *>(ctx->perm.p),
+                    static_cast<const uint2 *>(ctx->rect_sorted.p),
+                    g.tight ? static_cast<const uint4 *>(ctx->rc_sorted.p) : nullptr, g.P,
+                    static_cast<const uint32_t *>(ctx->ds_ctl.p),
+                    static_cast<const uint32_t *>(ctx->col_hist.p),
+                    static_cast<uint32_t *>(ctx->digit_total.p), g.col_shift, tv_alt, cs,
+                    (uint32_t)cap, list_n),
+                "column scatter launch");
+        std::swap(tv, tv_alt);
+        if (g.col_shift < 32)
+            GSR_HIP(gsr_radix_sort_keys(&tv, &tv_alt, cap, g.col_shift, 32,
+                                        static_cast<uint32_t *>(ctx->hist.p),
+                                        static_cast<uint32_t *>(ctx->digit_total.p), cs, list_n),
+                    "tile sort launch");
+        e.point_list = tv;
+        return GSR_OK;
+    }, &e.main));
+    GSR_TRY(record_chain(ctx, [&](hipStream_t cs) -> int { return aux_chain(ctx, g, cs, fw); },
+                         &e.aux));
+    ++ctx->graph_records;
+    return GSR_OK;
+}
+
+// The recorded graphs of this frame's key (recording them on a miss), or nullptr on failure.
+int find_graphs(gsr_context *ctx, const Frame &f, GraphEntry **out) {
+    const GraphKey key = graph_key(ctx, f);
+    GraphEntry *hit = nullptr;
+    for (auto it = ctx->graph_cache.begin(); it != ctx->graph_cache.end();) {
+        if (it->key.ws_gen != ctx->ws_gen || it->key.cap != ctx->list_cap) {  // stale pointers
+            retire_graph(ctx, *it);
+            it = ctx->graph_cache.erase(it);
+            continue;
+        }
+        if (std::memcmp(&it->key, &key, sizeof(key)) == 0) hit = &*it;
+        ++it;
+    }
+    if (!hit) {
+        if (ctx->graph_cache.size() >= kGraphCache) {  // replace the least recently used
+            auto lru = std::min_element(ctx->graph_cache.begin(), ctx->graph_cache.end(),
+                                        [](const GraphEntry &a, const GraphEntry &b) {
+                                            return a.used < b.used;
+                                        });
+            retire_graph(ctx, *lru);
+            ctx->graph_cache.erase(lru);
+        }
+        GraphEntry e;
+        e.key = key;
+        const int rc = record_frame_graphs(ctx, f, e);
+        if (rc != GSR_OK) {
+            retire_graph(ctx, e);
+            return rc;
+        }
+        ctx->graph_cache.push_back(e);
+        hit = &ctx->graph_cache.back();
+    }
+    hit->used = ++ctx->graph_clock;
+    *out = hit;
+    return GSR_OK;
+}
+
+constexpr int kOverflow = 1;  // forward_graph: the list outgrew the capacity (not rendered)
+
+int forward_graph(gsr_context *ctx, Frame &f, const gsr_raster_settings *st, gsr_outputs *out) {
+    GraphEntry *e = nullptr;
+    GSR_TRY(find_graphs(ctx, f, &e));
+    hipStream_t s = f.s;
+    if (f.tmode == 1) GSR_HIP(hipEventRecord(f.ev[0], s), "hipEventRecord");
+    f.pa.frame_words = static_cast<uint32_t *>(ctx->frame_words.p);
+    GSR_HIP(gsr_launch_preprocess(f.pa, s), "preprocess launch");
+    GSR_HIP(hipEventRecord(ctx->fork, s), "hipEventRecord(fork)");
+    GSR_HIP(hipGraphLaunch(e->main, s), "hipGraphLaunch(frame stream)");
+    GSR_HIP(hipStreamWaitEvent(ctx->aux, ctx->fork, 0), "hipStreamWaitEvent(fork)");
+    GSR_HIP(hipGraphLaunch(e->aux, ctx->aux), "hipGraphLaunch(second stream)");
+    GSR_HIP(hipEventRecord(ctx->join, ctx->aux), "hipEventRecord(join)");
+    GSR_HIP(hipStreamWaitEvent(s, ctx->join, 0), "hipStreamWaitEvent(join)");
+    GSR_TRY(stage_end(ctx, f, 5));
+    f.point_list = e->point_list;
+    f.tiles_local = nullptr;
+    f.id_mask = f.col_shift < 32 ? (1u << f.col_shift) - 1u : 0xFFFFFFFFu;
+    GSR_TRY(launch_blend(ctx, f, st, out));
+    GSR_TRY(stage_end(ctx, f, 6));
+    ++ctx->graph_frames;
+    // K for num_rendered: published by the first kernel after the preprocess, long before the
+    // host has queued the rest of the frame
+    uint64_t tagv = 0;
+    if (!spin_on(&ctx->h_total[7], [&](uint64_t v) { return v == f.tag; }, tagv))
+        GSR_HIP(hipStreamSynchronize(f.main_publish ? s : ctx->aux),
+                "hipStreamSynchronize(pair count)");
+    f.K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
+    ctx->last_D = (uint32_t)__atomic_load_n(&ctx->h_total[3], __ATOMIC_ACQUIRE);
+    f.KL = f.tight ? __atomic_load_n(&ctx->h_total[5], __ATOMIC_ACQUIRE) : f.K;
+    if (f.K > (uint64_t)UINT32_MAX - 4096)
+        return fail(GSR_E_INVALID, "gsr_forward: more than 2^32-4097 (Gaussian, tile) pairs");
+    if ((int64_t)f.KL > ctx->list_cap) return kOverflow;
+    finish_frame(ctx, f, out);
+    return GSR_OK;
+}
+
 int forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings *st,
             gsr_outputs *out, hipStream_t s) {
     Frame f;
     ctx->have_forward = false;
     GSR_TRY(setup_frame(ctx, g, st, out, s, f));
+    f.graph = f.P > 0 && graph_eligible(ctx, f, out);
+    if (f.graph) {
+        GSR_TRY(drain_retired(ctx, s, false));
+        const int rc = forward_graph(ctx, f, st, out);
+        if (rc != kOverflow) return rc;
+        // the list outgrew the capacity: nothing was binned or blended.  Grow the capacity and
+        // render the frame again the direct way (the stream orders it after the skipped one)
+        ++ctx->graph_overflows;
+        ctx->list_cap = list_capacity((int64_t)f.KL, ctx->list_cap);
+        GSR_TRY(reserve_K(ctx, ctx->list_cap, s));
+        GSR_TRY(setup_frame(ctx, g, st, out, s, f));
+        f.graph = false;
+    }
 
     if (f.P == 0) {  // upstream returns the zero-initialised image without rendering
         GSR_HIP(hipMemsetAsync(out->color, 0, (size_t)3 * f.rows_out * f.W * sizeof(float), s),
@@ -725,18 +1046,7 @@ int forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings 
     // ---- 7. blend
     GSR_TRY(launch_blend(ctx, f, st, out));
     GSR_TRY(stage_end(ctx, f, 6));
-
-    out->num_rendered = (int64_t)f.K;
-    ctx->last_K = (int64_t)f.K;
-    ctx->last_list = (int64_t)f.KL;
-    ctx->last_tight = f.tight;
-    ctx->last_gx = f.gx, ctx->last_gy = f.gy, ctx->last_rb = f.rb, ctx->last_re = f.re;
-    ctx->last_point_list = f.point_list;
-    ctx->last_tiles_local = f.tiles_local;
-    ctx->last_id_mask = f.id_mask;
-    ctx->last_packed = f.colpairs && f.KL > 0;
-    ctx->have_forward = true;
-    if (f.tmode) ++ctx->timed_frames;
+    finish_frame(ctx, f, out);
     return GSR_OK;
 }
 
@@ -778,6 +1088,9 @@ int gsr_create(gsr_context **out) {
     }
     bool ok = hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking, prio_least) ==
                   hipSuccess &&
+              hipStreamCreateWithFlags(&ctx->cap_stream, hipStreamNonBlocking) == hipSuccess &&
+              hipMalloc(&ctx->frame_words.p, 64) == hipSuccess &&
+              hipMemset(ctx->frame_words.p, 0, 64) == hipSuccess &&
               // stream-to-stream hand-offs on one device: a device-scope release suffices
               hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming | hipEventReleaseToDevice) ==
                   hipSuccess &&
@@ -802,13 +1115,16 @@ int gsr_create(gsr_context **out) {
 void gsr_destroy(gsr_context *ctx) {
     if (!ctx) return;
     (void)hipDeviceSynchronize();
+    for (GraphEntry &e : ctx->graph_cache) retire_graph(ctx, e);
+    for (hipGraphExec_t ge : ctx->graph_retired) (void)hipGraphExecDestroy(ge);
     DevBuf *bufs[] = {&ctx->records,     &ctx->strip_rect,    &ctx->sort_keys,  &ctx->ds_a,
                       &ctx->ds_b,        &ctx->block_kept,    &ctx->partials,   &ctx->total,
                       &ctx->hist,        &ctx->digit_total,   &ctx->bin,        &ctx->chunk_first,
                       &ctx->rect_sorted, &ctx->pair_count,    &ctx->perm,       &ctx->ds_ctl,
                       &ctx->tile_keys,   &ctx->tile_vals,     &ctx->tile_keys_alt,
                       &ctx->tile_vals_alt, &ctx->ranges_local, &ctx->tile_diff, &ctx->col_hist,
-                      &ctx->color_ids, &ctx->blend_order, &ctx->strip_rc, &ctx->rc_sorted};
+                      &ctx->color_ids, &ctx->blend_order, &ctx->strip_rc, &ctx->rc_sorted,
+                      &ctx->frame_words};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &set : ctx->ev)
@@ -821,6 +1137,7 @@ void gsr_destroy(gsr_context *ctx) {
     if (ctx->join) (void)hipEventDestroy(ctx->join);
     if (ctx->compacted) (void)hipEventDestroy(ctx->compacted);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
+    if (ctx->cap_stream) (void)hipStreamDestroy(ctx->cap_stream);
     if (ctx->h_total) (void)hipHostFree(ctx->h_total);
     delete ctx;
 }
@@ -828,7 +1145,9 @@ void gsr_destroy(gsr_context *ctx) {
 int gsr_reserve(gsr_context *ctx, int64_t P, int64_t K) {
     if (!ctx || P < 0 || K < 0) return fail(GSR_E_INVALID, "gsr_reserve: bad arguments");
     GSR_TRY(reserve_P(ctx, P, nullptr));
-    GSR_TRY(reserve_K(ctx, K, nullptr));
+    if (K > ctx->list_cap) ctx->list_cap = std::min<int64_t>((K + 4095) & ~(int64_t)4095,
+                                                             (int64_t)UINT32_MAX - 4096);
+    GSR_TRY(reserve_K(ctx, std::max<int64_t>(K, ctx->list_cap), nullptr));
     GSR_HIP(hipDeviceSynchronize(), "gsr_reserve");
     return GSR_OK;
 }
@@ -842,6 +1161,7 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
             ctx->fast = (int)value;
             return GSR_OK;
         case GSR_OPT_TIGHT_BINNING: ctx->tight = value ? 1 : 0; return GSR_OK;
+        case GSR_OPT_FRAME_GRAPHS: ctx->graphs = value ? 1 : 0; return GSR_OK;
         case GSR_OPT_DEPTH_SORT:
             if (value < -1 || value > 3)
                 return fail(GSR_E_INVALID, "gsr_set_option: depth sort -1..3");
@@ -850,6 +1170,14 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
         default:
             return fail(GSR_E_INVALID, "gsr_set_option: unknown option " + std::to_string(option));
     }
+}
+
+int gsr_frame_graph_stats(gsr_context *ctx, int64_t *stats, int n) {
+    if (!ctx || (!stats && n > 0)) return fail(GSR_E_INVALID, "gsr_frame_graph_stats: bad arguments");
+    const int64_t v[4] = {ctx->graph_frames, ctx->graph_records, ctx->graph_overflows,
+                          ctx->list_cap};
+    for (int i = 0; i < n && i < 4; ++i) stats[i] = v[i];
+    return 4;
 }
 
 int gsr_set_timing(gsr_context *ctx, int enable) {
@@ -897,7 +1225,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
 }
 
 int gsr_get_binning(gsr_context *ctx, uint32_t *point_list, uint32_t *point_tiles,
-                    uint32_t *ranges, int64_t *num_rendered, int32_t *num_tiles, void *stream) {
+                    uint32_t *ranges, int64_t *list_entries, int32_t *num_tiles, void *stream) {
     if (!ctx) return fail(GSR_E_INVALID, "gsr_get_binning: NULL context");
     if (!ctx->have_forward) return fail(GSR_E_STATE, "gsr_get_binning: no forward yet");
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -905,7 +1233,7 @@ int gsr_get_binning(gsr_context *ctx, uint32_t *point_list, uint32_t *point_tile
     const uint64_t T = (uint64_t)ctx->last_gx * ctx->last_gy;
     const uint64_t off = (uint64_t)ctx->last_rb * ctx->last_gx;
     const uint64_t T_strip = (uint64_t)ctx->last_gx * (ctx->last_re - ctx->last_rb);
-    if (num_rendered) *num_rendered = K;
+    if (list_entries) *list_entries = K;  // (tight lists: fewer than the forward's num_rendered)
     if (num_tiles) *num_tiles = (int32_t)T;
     if (point_list && K > 0) {
         if (ctx->last_id_mask != 0xFFFFFFFFu)

@@ -514,13 +514,20 @@ __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict_
                                                      const uint32_t *__restrict__ hist, int64_t ng,
                                                      const uint32_t *__restrict__ off,
                                                      const uint32_t *__restrict__ digit_total,
-                                                     int pack_shift, uint32_t *__restrict__ out) {
+                                                     int pack_shift, uint32_t *__restrict__ out,
+                                                     uint32_t cap, uint32_t *__restrict__ list_n) {
     __shared__ ColScatterSmem c;
     __shared__ union {
         RadixTileSmem<kCW, kCIt> big;
         RadixTileSmem<kCW, kCIt / 2> small;
     } sm;
     const int tid = threadIdx.x;
+    // global start of column d for this block's segments: all earlier columns (then earlier
+    // blocks, below); the total is the list length
+    uint32_t tot;
+    const uint32_t dstart = block256_exclusive_scan(digit_total[tid], c.tmp, tot);
+    if (list_n && blockIdx.x == 0 && tid == 0) *list_n = tot;  // (frame graphs: the row pass)
+    if (tot > cap) return;  // (frame graphs) the list does not fit: the host re-renders
     const int64_t n = *d_n;
     const int64_t base = (int64_t)blockIdx.x * kCG;
     if (base >= n) return;
@@ -539,9 +546,6 @@ __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict_
     c.cols_lo[tid] = q.x;
     c.cols_hi[tid] = q.y;
     c.id[tid] = valid ? perm[e] : 0u;
-    uint32_t tot;
-    // global start of column d for this block: all earlier columns, then earlier blocks
-    const uint32_t dstart = block256_exclusive_scan(digit_total[tid], c.tmp, tot);
     c.colbase[tid] = dstart + hist[(int64_t)tid * ng + blockIdx.x / kCGroup] +
                      off[(int64_t)blockIdx.x * kRadixBins + tid];
     // thread t owns segments [seg0, seg0 + w) (one per column of its rect)
@@ -935,11 +939,11 @@ hipError_t gsr_launch_col_pairs_scatter(const uint32_t *perm, const uint2 *rect_
                                         const uint4 *rc_sorted, int64_t n_max,
                                         const uint32_t *d_n, const uint32_t *hist,
                                         const uint32_t *digit_total, int pack_shift, uint32_t *out,
-                                        hipStream_t s) {
+                                        hipStream_t s, uint32_t cap, uint32_t *list_n) {
     const int64_t nb = (n_max + kCG - 1) / kCG, ng = (nb + kCGroup - 1) / kCGroup;
     if (nb == 0) return hipSuccess;
     const uint32_t *off = hist + ng * kRadixBins;
     hipLaunchKernelGGL(k_col_scatter, dim3((unsigned)nb), dim3(kCG), 0, s, perm, rect_sorted,
-                       rc_sorted, d_n, hist, ng, off, digit_total, pack_shift, out);
+                       rc_sorted, d_n, hist, ng, off, digit_total, pack_shift, out, cap, list_n);
     return hipGetLastError();
 }

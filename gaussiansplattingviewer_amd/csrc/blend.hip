@@ -165,6 +165,7 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
     const uint32_t b = blockIdx.x;
     const uint32_t work = xcd_work(b, a.order, (n_work + kXcdGroup - 1) / kXcdGroup);
     if (work >= n_work) return;
+    if (a.list_n && *a.list_n > a.list_cap) return;  // not binned (frame graphs: re-rendered)
     const int lane = threadIdx.x;
     const uint32_t tile = work >> 2, quad = work & 3u;
     const uint32_t tx = tile % a.grid_x, ty_local = tile / a.grid_x, ty = a.row_begin + ty_local;

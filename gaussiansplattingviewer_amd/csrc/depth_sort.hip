@@ -47,8 +47,11 @@ static_assert(kDSubBins * kDW == kDThreads, "one thread per (sub-digit, wave) in
 constexpr int kDPer = kDBins / kDThreads;  // digit starts per thread in the prologue
 static_assert(kDPer == 8, "two 16-B loads of digit totals and of the hist row per thread");
 
-// ctl: [0] kept count, [1] D (key bits to sort), [2..3] unused, then per tile uint4 {OR, AND,
-// kept, 0} of pass 0.
+// ctl: [0] kept count, [1] D (key bits to sort), [2] the MSD pass's shift (D - 12, or 0 when
+// D <= 12; written by k_ds_bits or gsr_launch_count_pairs before the MSD pass), [3] unused, then
+// per tile uint4 {OR, AND, kept, 0} of pass 0.  The MSD kernels read only ctl[2]: the LSD form's
+// pass-0 scan also rewrites ctl[1] from the sort's own tiles (in the MSD form a diagnostic that
+// debug forwards compare with the preprocess's D, api.hip wait_K).
 constexpr int kCtlHead = 4;
 
 __device__ __forceinline__ int pass_bits(int shift) { return min(kDBits, 32 - shift); }
@@ -341,8 +344,8 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
     const int64_t base = (int64_t)blockIdx.x * kDT;
     if (base >= n) return;
     const int nbits = pass_bits(shift);
-    // msd: the pass sorted the top digit; it is the whole sort only when D <= 12
-    const bool last = (kFirst && msd) ? D <= (uint32_t)kDBits
+    // msd: the pass sorted the top digit; it is the whole sort only when D <= 12 (shift 0)
+    const bool last = (kFirst && msd) ? ctl[2] == 0u
                                       : shift + nbits >= 32 || D <= (uint32_t)(shift + nbits);
     const uint32_t nbins = 1u << nbits, mask = nbins - 1u;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -771,9 +774,9 @@ __global__ __launch_bounds__(kDThreads) void k_ds_local(uint2 *__restrict__ pair
                                                         const uint32_t *__restrict__ ctl,
                                                         const uint32_t *__restrict__ digit_total) {
     __shared__ LocalSmem sm;
-    const uint32_t D = ctl[1];
-    if (D <= (uint32_t)kDBits) return;
-    const int low = (int)(D - (uint32_t)kDBits);  // bits below the MSD digit
+    // the bits below the MSD digit: the MSD pass's own shift (ctl[2]); 0 when D <= 12
+    const int low = (int)ctl[2];
+    if (low == 0) return;
     const uint32_t shift_hi = (uint32_t)low;
     const int tid = threadIdx.x, w = tid >> 6;
     const uint32_t d0 = blockIdx.x * kLGroup;

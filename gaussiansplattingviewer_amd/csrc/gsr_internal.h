@@ -250,11 +250,18 @@ struct GsrPreprocessArgs {
     // pinned host memory (device-mapped): [K, D, -, K over the spans, -, K tag]
     unsigned long long *host_K;
     uint32_t k_tag;              // nonzero: stored to host_K[5] after K (the host spins on it)
+    // frame graphs (api.hip): device words of the context -- [0] the frame's tag, [4..6] the
+    // camera position -- which k_preprocess's block 0 stores (k_tag, *campos) for the kernels of
+    // a recorded graph, whose arguments cannot change per frame; NULL otherwise
+    uint32_t *frame_words;
     // optional debug outputs
     float *depths, *means2D, *conic_opacity, *rgb;
     uint32_t *tiles_touched;
 };
 
+// k_preprocess blocks of 256 Gaussians: the count of GsrPreprocessArgs.block_pairs entries and
+// of the kept-key OR / AND words after them (the one definition every reader of them uses).
+inline int64_t gsr_preprocess_blocks(int64_t P) { return (P + 255) / 256; }
 hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, hipStream_t s);
 // SH -> RGB (or colors_precomp) of every Gaussian with radii > 0 into SplatRecord.c.yzw (+ rgb).
 // waves_per_simd (1..7): cap on the colour waves a CU holds at once (0 = no cap).
@@ -269,8 +276,10 @@ hipError_t gsr_launch_color_ids(const GsrPreprocessArgs &a, const uint32_t *ids,
 // depth sort's control words, ctl[1] = D and ctl[2] = its pass's shift (gsr_depth_sort_msd
 // with keybits NULL), so the publish runs on the main stream in place of the sort's own
 // key-bit reduction.
+// d_tag (frame graphs): the tag is read from this device word (k_preprocess's frame_words[0])
+// instead of a.k_tag.
 hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s,
-                                  uint32_t *ds_ctl = nullptr);
+                                  uint32_t *ds_ctl = nullptr, const uint32_t *d_tag = nullptr);
 hipError_t gsr_launch_mark_visible(const float *means3D, int64_t P, const float *viewmatrix,
                                    uint8_t *visible, hipStream_t s);
 hipError_t gsr_launch_view_depth_keys(const float *xyz, int64_t P, float v20, float v21, float v22,
@@ -287,8 +296,12 @@ hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **key
                                 uint32_t *hist, uint32_t *digit_total, hipStream_t s,
                                 int first_pass = 0);
 // The same for keys alone (the column-first binning's row pass over packed pair words).
+// d_n (frame graphs): the element count is *d_n, read on the device; n is then the capacity
+// the grids, the buffers and hist are sized for, and a count above it sorts nothing (the host
+// re-renders such a frame, api.hip).
 hipError_t gsr_radix_sort_keys(uint32_t **keys, uint32_t **keys_alt, int64_t n, int begin_bit,
-                               int end_bit, uint32_t *hist, uint32_t *digit_total, hipStream_t s);
+                               int end_bit, uint32_t *hist, uint32_t *digit_total, hipStream_t s,
+                               const uint32_t *d_n = nullptr);
 // k_rs_scan alone: per digit, exclusive scan of hist[d][0..nb) across tiles -> digit_total[d].
 hipError_t gsr_launch_digit_scan(uint32_t *hist, int64_t nb, uint32_t *digit_total,
                                  hipStream_t s);
@@ -383,11 +396,14 @@ hipError_t gsr_launch_col_pairs_count(const uint32_t *perm, const uint2 *strip_r
                                       const uint4 *strip_rc, int64_t n_max, const uint32_t *d_n,
                                       uint2 *rect_sorted, uint4 *rc_sorted, uint32_t *hist,
                                       uint32_t *digit_total, hipStream_t s);
+// list_n (frame graphs, else NULL): the list length (the column totals' sum) is stored there
+// for the row pass; a list longer than cap is not written (the host re-renders the frame).
 hipError_t gsr_launch_col_pairs_scatter(const uint32_t *perm, const uint2 *rect_sorted,
                                         const uint4 *rc_sorted, int64_t n_max,
                                         const uint32_t *d_n, const uint32_t *hist,
                                         const uint32_t *digit_total, int pack_shift, uint32_t *out,
-                                        hipStream_t s);
+                                        hipStream_t s, uint32_t cap = 0xFFFFFFFFu,
+                                        uint32_t *list_n = nullptr);
 hipError_t gsr_launch_digit_scan_n(uint32_t *hist, int64_t nb, uint32_t *digit_total,
                                    const uint32_t *d_n, int64_t tile, hipStream_t s);
 // Packed pair lists (column-first binning): ids = packed & mask; tile ids (offset + strip-local
@@ -433,6 +449,11 @@ struct GsrBlendArgs {
     int fast;            // 1: folded-constant FMA arithmetic + raw v_exp_f32; 0: upstream order
     uint32_t id_mask;    // point_list word -> Gaussian id (packed pair lists; else ~0u)
     const uint32_t *order;  // tile groups heaviest first (gsr_launch_blend_order), or nullptr
+    // frame graphs: the list length on the device (k_col_scatter) and the capacity the list was
+    // binned into; a longer list was not binned, so the blend writes nothing (the host
+    // re-renders the frame).  NULL: the host sized the list.
+    const uint32_t *list_n;
+    uint32_t list_cap;
 };
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s);
 // The blend's dispatch order: the groups of 4 row-adjacent tiles (16 quadrant waves, one XCD)

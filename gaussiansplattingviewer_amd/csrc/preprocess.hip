@@ -490,6 +490,14 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+        if (a.frame_words && blockIdx.x == 0) {  // (frame graphs) this frame's tag and camera
+            a.frame_words[0] = a.k_tag;
+            if (a.campos) {
+                a.frame_words[4] = __float_as_uint(a.campos[0]);
+                a.frame_words[5] = __float_as_uint(a.campos[1]);
+                a.frame_words[6] = __float_as_uint(a.campos[2]);
+            }
+        }
         a.block_pairs[blockIdx.x] =
             ((uint64_t)(s_red[4][0] + s_red[4][1] + s_red[4][2] + s_red[4][3]) << 32) |
             (s_red[0][0] + s_red[0][1] + s_red[0][2] + s_red[0][3]);
@@ -509,7 +517,8 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
 __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__restrict__ cnt,
                                                     const uint2 *__restrict__ keybits, int64_t n,
                                                     unsigned long long *host_K,
-                                                    uint32_t k_tag, uint32_t *ds_ctl) {
+                                                    uint32_t k_tag, uint32_t *ds_ctl,
+                                                    const uint32_t *d_tag) {
     __shared__ unsigned long long s_w[16], s_wt[16];
     __shared__ uint32_t s_or[16], s_and[16];
     unsigned long long v = 0, vt = 0;
@@ -571,6 +580,7 @@ __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__
         __hip_atomic_store(host_K, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         // the host spins on this tag instead of sleeping in an event wait (release: K and D are
         // visible first)
+        if (d_tag) k_tag = *d_tag;
         if (k_tag)
             __hip_atomic_store(host_K + 5, (unsigned long long)k_tag, __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_SYSTEM);
@@ -694,7 +704,7 @@ __global__ __launch_bounds__(256) void k_view_depth_keys(const float *__restrict
     if (depth_out) depth_out[idx] = d;
 }
 
-inline unsigned grid_for(int64_t n) { return (unsigned)((n + 255) / 256); }
+inline unsigned grid_for(int64_t n) { return (unsigned)gsr_preprocess_blocks(n); }
 
 }  // namespace
 
@@ -745,13 +755,14 @@ hipError_t gsr_launch_color_ids(const GsrPreprocessArgs &a, const uint32_t *ids,
     return hipGetLastError();
 }
 
-hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s, uint32_t *ds_ctl) {
+hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s, uint32_t *ds_ctl,
+                                  const uint32_t *d_tag) {
     if (a.P == 0) return hipSuccess;
     const unsigned g = grid_for(a.P);  // the preprocess's blocks
     const uint2 *keybits = reinterpret_cast<const uint2 *>(a.block_pairs + g);
     hipLaunchKernelGGL(k_publish_K, dim3(1), dim3(1024), 0, s,
                        reinterpret_cast<const unsigned long long *>(a.block_pairs), keybits,
-                       (int64_t)g, a.host_K, a.k_tag, ds_ctl);
+                       (int64_t)g, a.host_K, d_tag ? 0u : a.k_tag, ds_ctl, d_tag);
     return hipGetLastError();
 }
 

@@ -40,12 +40,23 @@ struct RsCount {
 // digit's kTiles counts as one word of 4 kTiles bytes: with one tile per block every 4-B store
 // lands on its own line (the 4K frame's upsweep wrote 278 MB for a 7 MB histogram), so large
 // passes take 4 tiles per block and write 16-B words (gsr_radix_hist_words pads the stride).
+// The element count of a pass whose count lives on the device (frame graphs): *d_n, or 0 when
+// it exceeds the capacity n_cap the launch was sized for (nothing is sorted; the host re-renders
+// the frame).  d_n NULL: n_cap itself.
+__device__ __forceinline__ int64_t live_count(const uint32_t *d_n, int64_t n_cap) {
+    if (!d_n) return n_cap;
+    const int64_t n = (int64_t)*d_n;
+    return n <= n_cap ? n : 0;
+}
+
 template <int kW, int kIt, int kTiles>
 __global__ __launch_bounds__(kW * 64) void k_rs_upsweep(const uint32_t *__restrict__ keys,
-                                                        int64_t n, int shift, uint32_t mask,
+                                                        int64_t n_cap, int shift, uint32_t mask,
                                                         uint32_t *__restrict__ hist,
-                                                        int64_t stride) {
+                                                        int64_t stride,
+                                                        const uint32_t *__restrict__ d_n) {
     constexpr int kThreads = kW * 64, kT = kThreads * kIt;
+    const int64_t n = live_count(d_n, n_cap);
     static_assert(kIt % 4 == 0, "full tiles are read as uint4");
     static_assert(kW >= 4, "the digit scans take one thread per digit (256)");
     static_assert(kTiles == 1 || kTiles == 4, "one tile or a 16-B word of four");
@@ -96,7 +107,8 @@ __global__ __launch_bounds__(kBlock) void k_rs_scan(uint32_t *__restrict__ hist,
                                                     uint32_t *__restrict__ digit_total,
                                                     const RsCount cnt, int64_t kT) {
     __shared__ uint32_t s_tmp[4];
-    const int64_t nb_act = cnt.d_n ? ((int64_t)*cnt.d_n + kT - 1) / kT : cnt.n_host;
+    const int64_t nb_act =
+        cnt.d_n ? min(((int64_t)*cnt.d_n + kT - 1) / kT, cnt.n_host) : cnt.n_host;
     uint32_t *h = hist + (int64_t)blockIdx.x * stride;
     uint32_t carry = 0;
     const bool vec = (stride & 3) == 0;  // 16-B aligned columns: whole words of 4 tiles
@@ -134,10 +146,11 @@ __global__ __launch_bounds__(kBlock) void k_rs_scan(uint32_t *__restrict__ hist,
 template <int kW, int kIt, bool kVals>
 __global__ __launch_bounds__(kW * 64) void k_rs_downsweep(
     const uint32_t *__restrict__ keys_in, const uint32_t *__restrict__ vals_in,
-    uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out, int64_t n,
+    uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out, int64_t n_cap,
     int shift, int nbits, const uint32_t *__restrict__ hist,
-    const uint32_t *__restrict__ digit_total, int64_t nb) {
+    const uint32_t *__restrict__ digit_total, int64_t nb, const uint32_t *__restrict__ d_n) {
     constexpr int kT = kW * 64 * kIt;
+    const int64_t n = live_count(d_n, n_cap);
     __shared__ uint32_t s_keys[kT];
     __shared__ uint32_t s_vals[kVals ? kT : 1];
     __shared__ RadixTileSmem<kW, kIt> sm;
@@ -208,27 +221,31 @@ int64_t gsr_radix_hist_words(int64_t n) {
     return (nb < 1 ? 4 : hist_stride(nb)) * kRadix;
 }
 
-// One pass: upsweep, scan, downsweep.  v == nullptr: keys only.
+// One pass: upsweep, scan, downsweep.  v == nullptr: keys only.  d_n: the count on the device
+// (n the capacity; live_count).
 static void rts_pass(const uint32_t *k, const uint32_t *v, uint32_t *ko, uint32_t *vo, int64_t n,
-                     int shift, int nbits, uint32_t *hist, uint32_t *digit_total, hipStream_t s) {
+                     int shift, int nbits, uint32_t *hist, uint32_t *digit_total, hipStream_t s,
+                     const uint32_t *d_n = nullptr) {
     const int64_t nb = (n + kST - 1) / kST;  // tiles: the downsweep's grid
     if (nb == 0) return;
     const int64_t stride = hist_stride(nb);
     const uint32_t mask = (1u << nbits) - 1u;
     if (nb >= kQuadTiles)
         hipLaunchKernelGGL((k_rs_upsweep<kSW, kSIt, 4>), dim3((unsigned)((nb + 3) / 4)),
-                           dim3(kSW * 64), 0, s, k, n, shift, mask, hist, stride);
+                           dim3(kSW * 64), 0, s, k, n, shift, mask, hist, stride, d_n);
     else
         hipLaunchKernelGGL((k_rs_upsweep<kSW, kSIt, 1>), dim3((unsigned)nb), dim3(kSW * 64), 0, s,
-                           k, n, shift, mask, hist, stride);
+                           k, n, shift, mask, hist, stride, d_n);
+    // (with d_n, an over-capacity count scans stale counts, in bounds; the downsweep then
+    // sorts nothing)
     hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, stride, digit_total,
-                       RsCount{nb, nullptr}, kST);
+                       RsCount{nb, d_n}, kST);
     if (v)
         hipLaunchKernelGGL((k_rs_downsweep<kSW, kSIt, true>), dim3((unsigned)nb), dim3(kSW * 64), 0,
-                           s, k, v, ko, vo, n, shift, nbits, hist, digit_total, stride);
+                           s, k, v, ko, vo, n, shift, nbits, hist, digit_total, stride, d_n);
     else
         hipLaunchKernelGGL((k_rs_downsweep<kSW, kSIt, false>), dim3((unsigned)nb), dim3(kSW * 64),
-                           0, s, k, v, ko, vo, n, shift, nbits, hist, digit_total, stride);
+                           0, s, k, v, ko, vo, n, shift, nbits, hist, digit_total, stride, d_n);
 }
 
 hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **keys_alt,
@@ -247,12 +264,13 @@ hipError_t gsr_radix_sort_pairs(uint32_t **keys, uint32_t **vals, uint32_t **key
 }
 
 hipError_t gsr_radix_sort_keys(uint32_t **keys, uint32_t **keys_alt, int64_t n, int begin_bit,
-                               int end_bit, uint32_t *hist, uint32_t *digit_total, hipStream_t s) {
-    if (n <= 1) return hipSuccess;
+                               int end_bit, uint32_t *hist, uint32_t *digit_total, hipStream_t s,
+                               const uint32_t *d_n) {
+    if (n <= 1 && !d_n) return hipSuccess;
     const GsrRadixPlan plan = gsr_radix_plan(begin_bit, end_bit);
     for (int p = 0; p < plan.n; ++p) {
         rts_pass(*keys, nullptr, *keys_alt, nullptr, n, plan.shift[p], plan.nbits[p], hist,
-                 digit_total, s);
+                 digit_total, s, d_n);
         std::swap(*keys, *keys_alt);
     }
     return hipGetLastError();

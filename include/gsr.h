@@ -26,7 +26,8 @@
  *   - `stream` is a hipStream_t (NULL = the default stream); all work is enqueued on it.
  *     gsr_forward waits once per call for the number of (Gaussian, tile) pairs, as upstream
  *     does for num_rendered -- not for the stream: the GPU stores it into pinned memory as
- *     soon as the preprocess has counted it, while the depth sort runs;
+ *     soon as the preprocess has counted it, while the depth sort runs.  With frame graphs
+ *     (GSR_OPT_FRAME_GRAPHS) that wait comes after the whole frame is queued;
  *   - every function returns GSR_OK (0) or a negative GSR_E* code; gsr_last_error()
  *     returns the calling thread's last message.  The Python layer raises RuntimeError.
  */
@@ -123,7 +124,8 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
                 gsr_outputs *out, void *stream);
 
 /* Binning state of the last gsr_forward on this context: the pair lists its blend read.  Writes
- * the sizes (K list entries, T tiles of the whole frame) and, for each non-NULL caller-owned
+ * the sizes (list_entries = K, the entries of the lists; num_tiles = T, tiles of the whole
+ * frame) and, for each non-NULL caller-owned
  * DEVICE buffer, copies: point_list[K] Gaussian ids sorted by (tile, depth); point_tiles[K]
  * their global tile ids; ranges[2*T] = [start,end) per tile (tiles outside the strip stay 0,0,
  * as upstream's memset leaves unused tiles).  With upstream's lists (GSR_OPT_TIGHT_BINNING 0, a
@@ -132,7 +134,7 @@ int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
  * subsequence of upstream's: tests/test_gpu_tight_pin.py checks that against the oracle).  Call
  * once with NULL buffers to size them.  Synchronises `stream`. */
 int gsr_get_binning(gsr_context *ctx, uint32_t *point_list, uint32_t *point_tiles,
-                    uint32_t *ranges, int64_t *num_rendered, int32_t *num_tiles, void *stream);
+                    uint32_t *ranges, int64_t *list_entries, int32_t *num_tiles, void *stream);
 
 /* Per tile row of the last gsr_forward's strip, its (Gaussian, tile) pair count:
  * row_pairs[r] for r < n_rows = tile_row_end - tile_row_begin (DEVICE buffer, written on
@@ -221,6 +223,14 @@ const char *gsr_stage_name(int i);
  *     after the compaction.  auto = the compaction on strips (a proper subset of the tile rows)
  *     of >= 4M Gaussians, the MSD form when the previous frame's kept keys differed in <= 24
  *     bits (3 or 2), else the LSD passes (1 or 0).  Every form gives the same permutation.
+ *   GSR_OPT_FRAME_GRAPHS (default 0): the chains of the frame after the preprocess (the frame
+ *     stream's: K, depth sort, binning; the second stream's: tile ranges, blend order, colour)
+ *     are recorded once per context and key (input pointers, sizes, strip, workspace) as two
+ *     linear HIP graphs and replayed, the binning sized by a capacity (the list lengths seen
+ *     so far + 25 %) instead of a mid-frame wait for K; a frame whose list outgrows it is
+ *     rendered again the direct way after the capacity grows.  Used for column-first frames
+ *     without debug, per-stage timing (gsr_set_timing 1), the compacting depth sort or the rgb
+ *     output; the image and every output are the same as with 0.
  *   GSR_OPT_TIGHT_BINNING (default 1): with the column-first form and no n_contrib output, each
  *     Gaussian of a rect up to 8 tile columns x 15 rows is paired only with the tiles its
  *     alpha >= 1/255 ellipse reaches (upstream's blend skips it on the others), so the lists are
@@ -233,8 +243,13 @@ const char *gsr_stage_name(int i);
  * columns and strip rows, else the per-pair form; both produce the same lists.  Ids 10 and 12
  * are retired (ABI 1's column-pairs and tight-binning options) and rejected. */
 enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_DEPTH_SORT = 11,
-       GSR_OPT_TIGHT_BINNING = 13 };
+       GSR_OPT_TIGHT_BINNING = 13, GSR_OPT_FRAME_GRAPHS = 14 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
+
+/* Frame-graph counters of a context: stats[0] forwards rendered by replaying graphs,
+ * stats[1] graph pairs recorded, stats[2] forwards re-rendered after the list outgrew the
+ * capacity, stats[3] the current list capacity.  Writes min(n, 4); returns 4. */
+int gsr_frame_graph_stats(gsr_context *ctx, int64_t *stats, int n);
 
 #ifdef __cplusplus
 }

@@ -478,6 +478,20 @@ void oracle_render(const OracleIn *in, const uint32_t *ranges, const uint32_t *p
         }
 }
 
+/* forward.cu computeColorFromSH over P Gaussians (every one, not only the visible): rgb[3P]
+ * the clamped colour, clamped[3P] (optional) its clamp flags -- so the pre-clamp value is rgb
+ * where the flag is 0.  For the GLSL-twin check (tests/test_oracle_glsl_twins.py). */
+void oracle_color_from_sh(int64_t P, int deg, int max_coeffs, const float *means,
+                          const float *campos, const float *shs, float *rgb, uint8_t *clamped) {
+    for (int64_t i = 0; i < P; ++i)
+        compute_color_from_sh(i, deg, max_coeffs, means, campos, shs, clamped, rgb + 3 * i);
+}
+
+/* forward.cu computeCov3D over P Gaussians: cov3d[6P] (xx, xy, xz, yy, yz, zz). */
+void oracle_cov3d(int64_t P, const float *scales, float mod, const float *rots, float *cov3d) {
+    for (int64_t i = 0; i < P; ++i) compute_cov3d(scales + 3 * i, mod, rots + 4 * i, cov3d + 6 * i);
+}
+
 /* Threads of the parallel loops above (< 1: back to OpenMP's initial default, e.g.
  * OMP_NUM_THREADS); returns the count in effect. */
 int oracle_set_threads(int n) {

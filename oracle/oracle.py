@@ -71,6 +71,10 @@ def lib() -> ctypes.CDLL:
         L.oracle_tight_model_check.restype = i64
         L.oracle_tight_model_check.argtypes = [i64, vp, vp, vp, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_float, vp]
+        L.oracle_color_from_sh.restype = None
+        L.oracle_color_from_sh.argtypes = [i64, ctypes.c_int, ctypes.c_int] + [vp] * 5
+        L.oracle_cov3d.restype = None
+        L.oracle_cov3d.argtypes = [i64, vp, ctypes.c_float, vp, vp]
         _lib = L
     return _lib
 
@@ -189,6 +193,29 @@ def tight_model_check(means2D, conic_opacity, radii, W, H, shrink=0.0) -> dict:
     lib().oracle_tight_model_check(len(r), _p(m2), _p(co), _p(r), int(W), int(H), float(shrink),
                                    _p(stats))
     return dict(zip(_MODEL_KEYS, (int(v) for v in stats)))
+
+
+def color_from_sh(means3D, campos, shs, sh_degree):
+    """upstream computeColorFromSH for every Gaussian: (rgb [P,3] clamped >= 0, clamped flags
+    [P,3] bool).  shs [P,M,3] or [P,3M]."""
+    means3D = _c(means3D).reshape(-1, 3)
+    P = means3D.shape[0]
+    shs = _c(shs).reshape(P, -1)
+    M = shs.shape[1] // 3
+    rgb = np.zeros((P, 3), np.float32)
+    clamped = np.zeros((P, 3), np.uint8)
+    lib().oracle_color_from_sh(P, int(sh_degree), M, _p(means3D), _p(_c(campos).reshape(3)),
+                               _p(shs), _p(rgb), _p(clamped))
+    return rgb, clamped.astype(bool)
+
+
+def cov3d(scales, rotations, scale_modifier=1.0) -> np.ndarray:
+    """upstream computeCov3D for every Gaussian: [P,6] upper triangle xx xy xz yy yz zz."""
+    scales = _c(scales).reshape(-1, 3)
+    rotations = _c(rotations).reshape(-1, 4)
+    out = np.zeros((scales.shape[0], 6), np.float32)
+    lib().oracle_cov3d(scales.shape[0], _p(scales), float(scale_modifier), _p(rotations), _p(out))
+    return out
 
 
 def view_depth(xyz, view) -> np.ndarray:

@@ -24,10 +24,14 @@ Captured:
                        (oracle/ply_oracle.read_vertex, numpy's parse of the PLY written from
                        the raw arrays); every line of load_ply after the parse is the
                        reference's own.
+  glsl_twins.npz    -- the numeric literals of the reference's GLSL twins of upstream's
+                       formulas (gau_vert.glsl:3-18 SH constants, the 1.3 clamp and 0.3
+                       low-pass of computeCov2D; gau_frag.glsl:21-27 alpha), parsed from the
+                       shader text (make_glsl_twins; --only glsl).
 Also writes oracle_c1.npz: the oracle's integer outputs for config C1 (a regression pin of the
 restatement, NOT a reference output -- the upstream CUDA forward is not available).
 
-Usage:  python tests/golden/make_golden.py [--only ply]
+Usage:  python tests/golden/make_golden.py [--only ply|camera_data|glsl]
 """
 from __future__ import annotations
 
@@ -126,9 +130,42 @@ def make_camera_data():
     print(f"wrote camera_data.npz ({len(rows)} poses)")
 
 
+def make_glsl_twins():
+    """The numeric literals of the reference's GLSL twins of the upstream formulas, parsed from
+    the shader text (numbers only, no source): gau_vert.glsl:3-18 (the SH basis constants, as
+    written with their `f` suffix), :101-102 (the 1.3 tan-fov clamp of computeCov2D), :117-118
+    (the 0.3 low-pass), and gau_frag.glsl:21-27 (the -0.5 of the exponent, the 0.99 alpha cap,
+    the 1/255 alpha floor).  tests/test_oracle_glsl_twins.py evaluates the GLSL formulas with
+    them and compares the oracle."""
+    import re
+    vert = open(os.path.join(REF, "shaders", "gau_vert.glsl")).read()
+    frag = open(os.path.join(REF, "shaders", "gau_frag.glsl")).read()
+    out = {}
+    for name, val in re.findall(r"#define\s+(SH_C\w+)\s+(-?[0-9.]+)f", vert):
+        out[name] = np.array(float(val), dtype=np.float64)
+    assert len(out) == 14, sorted(out)
+
+    def one(pattern, text, what):
+        m = re.findall(pattern, text)
+        assert len(set(m)) == 1, (what, m)
+        return np.array(float(m[0]), dtype=np.float64)
+
+    out["COV2D_CLAMP"] = one(r"lim[xy]\s*=\s*([0-9.]+)f\s*\*\s*tan_fov[xy]", vert, "clamp")
+    out["COV2D_LOWPASS"] = one(r"cov\[[01]\]\[[01]\]\s*\+=\s*([0-9.]+)f", vert, "low-pass")
+    out["ALPHA_EXP_COEF"] = one(r"power\s*=\s*(-[0-9.]+)f\s*\*", frag, "exponent")
+    out["ALPHA_CAP"] = one(r"min\(([0-9.]+)f,\s*alpha", frag, "alpha cap")
+    num, den = re.findall(r"opacity\s*<\s*([0-9.]+)f\s*/\s*([0-9.]+)f", frag)[0]
+    out["ALPHA_MIN"] = np.array(float(num) / float(den), dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, "glsl_twins.npz"), **out)
+    print("wrote glsl_twins.npz:", {k: float(v) for k, v in out.items()})
+
+
 def main(only=None):
     if only == "camera_data":
         make_camera_data()
+        return
+    if only == "glsl":
+        make_glsl_twins()
         return
     _stub_modules()
     sys.path.insert(0, REF)

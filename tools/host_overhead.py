@@ -22,6 +22,12 @@ xyz, rot, scale, opac = up(g.xyz), up(g.rot), up(g.scale), up(g.opacity)
 sh = up(g.sh).reshape(P, -1, 3).contiguous()
 view, proj, campos, tx, ty = cuda_camera_inputs(static_camera(W, H))
 view, proj, campos, bg = up(view), up(proj), up(campos), torch.zeros(3, device=dev)
+# GSR_GRAPHS=1: frame graphs on (GSR_OPT_FRAME_GRAPHS) for every slot
+from gaussiansplattingviewer_amd import _lib  # noqa: E402
+for _slot in (0, 1):
+    _lib.check(_lib.load_library().gsr_set_option(_lib.context(0, _slot), _lib.GSR_OPT_FRAME_GRAPHS,
+                                                   int(os.environ.get("GSR_GRAPHS", "0"))),
+               "gsr_set_option")
 for depth in (1, 2):
     pipe = FramePipeline(depth, dev)
     for it in range(2):
