@@ -86,6 +86,9 @@ def parse():
                          "the MSD pass + per-bucket local sort (auto: compact on strips of >= 4M "
                          "Gaussians, else MSD when the last frame's depth keys differed in <= 24 "
                          "bits, else LSD)")
+    ap.add_argument("--graphs", type=int, default=None, choices=[0, 1, 2],
+                    help="GSR_OPT_FRAME_GRAPHS for every context slot (default: the library's): "
+                         "0 direct, 1 recorded graphs, 2 the deferred-K chains launched directly")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU-oracle time to sample for cpu_baseline (whole frames; at least one)")
     return ap.parse_args()
@@ -419,6 +422,8 @@ def main():
         opt(_lib.GSR_OPT_BLEND_FAST, {"exact": 0, "fast": 1}[args.blend])
         opt(_lib.GSR_OPT_DEPTH_SORT,
             {"auto": -1, "lsd": 0, "compact": 1, "msd": 2, "compact-msd": 3}[args.depth_sort])
+        if args.graphs is not None:
+            opt(_lib.GSR_OPT_FRAME_GRAPHS, args.graphs)
 
     # The untimed diagnostic passes run first, so the device has been rendering for ~200 frames
     # when the timed region starts: a run of 20 timed frames after 5 warmup frames measured

@@ -101,7 +101,9 @@ struct GraphKey {
 
 struct GraphEntry {
     GraphKey key;
-    hipGraphExec_t main = nullptr, aux = nullptr;  // the frame stream's and the second stream's
+    // the frame stream's two halves (K publish + depth sort; column counts + binning) and the
+    // second stream's chain: queued in the direct path's order, sort, second stream, binning
+    hipGraphExec_t sort = nullptr, bin = nullptr, aux = nullptr;
     uint32_t *point_list = nullptr;                // the list the recorded row pass leaves
     uint64_t used = 0;                             // LRU stamp
 };
@@ -168,7 +170,6 @@ struct gsr_context {
     DevBuf frame_words;                  // [0] tag, [1] list length, [4..6] campos
     uint32_t ws_gen = 0;                 // bumped by every (re)allocation of a workspace buffer
     int64_t list_cap = 0;                // pair-list capacity of the graphs (0: none yet)
-    hipStream_t cap_stream = nullptr;    // private stream the graphs are recorded on
     std::vector<GraphEntry> graph_cache;
     std::vector<hipGraphExec_t> graph_retired;
     uint64_t graph_clock = 0;
@@ -809,9 +810,10 @@ GsrPreprocessArgs graph_args(const gsr_context *ctx, const GsrPreprocessArgs &a)
 }
 
 void retire_graph(gsr_context *ctx, GraphEntry &e) {
-    if (e.main) ctx->graph_retired.push_back(e.main);
-    if (e.aux) ctx->graph_retired.push_back(e.aux);
-    e.main = e.aux = nullptr;
+    for (hipGraphExec_t *ge : {&e.sort, &e.bin, &e.aux}) {
+        if (*ge) ctx->graph_retired.push_back(*ge);
+        *ge = nullptr;
+    }
 }
 
 // Destroys the retired executable graphs once enough have gathered (they ran only on this
@@ -826,10 +828,14 @@ int drain_retired(gsr_context *ctx, hipStream_t s, bool force) {
     return GSR_OK;
 }
 
-// Records one chain on the context's capture stream into an executable graph.
+// Records one chain into an executable graph, captured on the context's second stream (a
+// capture executes nothing; a private capture stream would take one of the process's
+// GPU_MAX_HW_QUEUES = 4 hardware queues, which the frame streams and second streams of two frames
+// in flight already fill: with it, every stream shares a queue and the direct path lost 20 % in
+// flight).
 template <typename Chain>
 int record_chain(gsr_context *ctx, Chain chain, hipGraphExec_t *out) {
-    hipStream_t cs = ctx->cap_stream;
+    hipStream_t cs = ctx->aux;
     GSR_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
     const int rc = chain(cs);
     hipGraph_t graph = nullptr;
@@ -845,44 +851,61 @@ int record_chain(gsr_context *ctx, Chain chain, hipGraphExec_t *out) {
     return GSR_OK;
 }
 
-// Records the frame's two chains (the key's) into e.
-int record_frame_graphs(gsr_context *ctx, const Frame &f, GraphEntry &e) {
+// The deferred-K frame's chains on stream cs (the frame graphs record them; GSR_OPT_FRAME_GRAPHS
+// 2 launches them directly): g is graph_frame's copy of the frame.
+Frame graph_frame(const gsr_context *ctx, const Frame &f) {
     Frame g = f;
     g.pa = graph_args(ctx, f.pa);
     g.tmode = 0;
-    const uint32_t *fw = static_cast<const uint32_t *>(ctx->frame_words.p);
+    return g;
+}
+
+// K publish (main-stream frames) + the depth sort.
+int chain_sort(gsr_context *ctx, Frame &g, hipStream_t cs) {
+    g.s = cs;
+    if (g.main_publish)
+        GSR_HIP(gsr_launch_count_pairs(g.pa, cs, static_cast<uint32_t *>(ctx->ds_ctl.p),
+                                       static_cast<const uint32_t *>(ctx->frame_words.p)),
+                "pair count launch");
+    return launch_depth_sort(ctx, g, 0, gsr_depth_sort_passes(32));
+}
+
+// The column counts, the column scatter and the row pass over the capacity, the list length
+// read on the device; *point_list: the buffer the sorted list ends in.
+int chain_bin(gsr_context *ctx, Frame &g, hipStream_t cs, uint32_t **point_list) {
+    g.s = cs;
+    GSR_TRY(launch_scan(ctx, g));
+    const int64_t cap = ctx->list_cap;
     uint32_t *list_n = static_cast<uint32_t *>(ctx->frame_words.p) + 1;
-    GSR_TRY(record_chain(ctx, [&](hipStream_t cs) -> int {
-        g.s = cs;
-        if (g.main_publish)
-            GSR_HIP(gsr_launch_count_pairs(g.pa, cs, static_cast<uint32_t *>(ctx->ds_ctl.p), fw),
-                    "pair count launch");
-        GSR_TRY(launch_depth_sort(ctx, g, 0, gsr_depth_sort_passes(32)));
-        GSR_TRY(launch_scan(ctx, g));
-        // the column scatter and the row pass over the capacity, the length read on the device
-        const int64_t cap = ctx->list_cap;
-        uint32_t *tv = static_cast<uint32_t *>(ctx->tile_vals.p);
-        uint32_t *tv_alt = static_cast<uint32_t *>(ctx->tile_vals_alt.p);
-        GSR_HIP(gsr_launch_col_pairs_scatter(
-                    static_cast<const uint32_t *>(ctx->perm.p),
-                    static_cast<const uint2 *>(ctx->rect_sorted.p),
-                    g.tight ? static_cast<const uint4 *>(ctx->rc_sorted.p) : nullptr, g.P,
-                    static_cast<const uint32_t *>(ctx->ds_ctl.p),
-                    static_cast<const uint32_t *>(ctx->col_hist.p),
-                    static_cast<uint32_t *>(ctx->digit_total.p), g.col_shift, tv_alt, cs,
-                    (uint32_t)cap, list_n),
-                "column scatter launch");
-        std::swap(tv, tv_alt);
-        if (g.col_shift < 32)
-            GSR_HIP(gsr_radix_sort_keys(&tv, &tv_alt, cap, g.col_shift, 32,
-                                        static_cast<uint32_t *>(ctx->hist.p),
-                                        static_cast<uint32_t *>(ctx->digit_total.p), cs, list_n),
-                    "tile sort launch");
-        e.point_list = tv;
-        return GSR_OK;
-    }, &e.main));
-    GSR_TRY(record_chain(ctx, [&](hipStream_t cs) -> int { return aux_chain(ctx, g, cs, fw); },
-                         &e.aux));
+    uint32_t *tv = static_cast<uint32_t *>(ctx->tile_vals.p);
+    uint32_t *tv_alt = static_cast<uint32_t *>(ctx->tile_vals_alt.p);
+    GSR_HIP(gsr_launch_col_pairs_scatter(
+                static_cast<const uint32_t *>(ctx->perm.p),
+                static_cast<const uint2 *>(ctx->rect_sorted.p),
+                g.tight ? static_cast<const uint4 *>(ctx->rc_sorted.p) : nullptr, g.P,
+                static_cast<const uint32_t *>(ctx->ds_ctl.p),
+                static_cast<const uint32_t *>(ctx->col_hist.p),
+                static_cast<uint32_t *>(ctx->digit_total.p), g.col_shift, tv_alt, cs,
+                (uint32_t)cap, list_n),
+            "column scatter launch");
+    std::swap(tv, tv_alt);
+    if (g.col_shift < 32)
+        GSR_HIP(gsr_radix_sort_keys(&tv, &tv_alt, cap, g.col_shift, 32,
+                                    static_cast<uint32_t *>(ctx->hist.p),
+                                    static_cast<uint32_t *>(ctx->digit_total.p), cs, list_n),
+                "tile sort launch");
+    *point_list = tv;
+    return GSR_OK;
+}
+
+// Records the frame's three chains (the key's) into e.
+int record_frame_graphs(gsr_context *ctx, const Frame &f, GraphEntry &e) {
+    Frame g = graph_frame(ctx, f);
+    const uint32_t *fw = static_cast<const uint32_t *>(ctx->frame_words.p);
+    GSR_TRY(record_chain(ctx, [&](hipStream_t cs) { return chain_sort(ctx, g, cs); }, &e.sort));
+    GSR_TRY(record_chain(ctx, [&](hipStream_t cs) { return chain_bin(ctx, g, cs, &e.point_list); },
+                         &e.bin));
+    GSR_TRY(record_chain(ctx, [&](hipStream_t cs) { return aux_chain(ctx, g, cs, fw); }, &e.aux));
     ++ctx->graph_records;
     return GSR_OK;
 }
@@ -928,19 +951,31 @@ constexpr int kOverflow = 1;  // forward_graph: the list outgrew the capacity (n
 
 int forward_graph(gsr_context *ctx, Frame &f, const gsr_raster_settings *st, gsr_outputs *out) {
     GraphEntry *e = nullptr;
-    GSR_TRY(find_graphs(ctx, f, &e));
+    const bool replay = ctx->graphs == 1;  // 2: the same chains launched directly
+    if (replay) GSR_TRY(find_graphs(ctx, f, &e));
+    Frame g = graph_frame(ctx, f);
+    const uint32_t *fw = static_cast<const uint32_t *>(ctx->frame_words.p);
     hipStream_t s = f.s;
     if (f.tmode == 1) GSR_HIP(hipEventRecord(f.ev[0], s), "hipEventRecord");
     f.pa.frame_words = static_cast<uint32_t *>(ctx->frame_words.p);
     GSR_HIP(gsr_launch_preprocess(f.pa, s), "preprocess launch");
     GSR_HIP(hipEventRecord(ctx->fork, s), "hipEventRecord(fork)");
-    GSR_HIP(hipGraphLaunch(e->main, s), "hipGraphLaunch(frame stream)");
+    if (replay) GSR_HIP(hipGraphLaunch(e->sort, s), "hipGraphLaunch(depth sort)");
+    else GSR_TRY(chain_sort(ctx, g, s));
     GSR_HIP(hipStreamWaitEvent(ctx->aux, ctx->fork, 0), "hipStreamWaitEvent(fork)");
-    GSR_HIP(hipGraphLaunch(e->aux, ctx->aux), "hipGraphLaunch(second stream)");
+    if (replay) GSR_HIP(hipGraphLaunch(e->aux, ctx->aux), "hipGraphLaunch(second stream)");
+    else GSR_TRY(aux_chain(ctx, g, ctx->aux, fw));
     GSR_HIP(hipEventRecord(ctx->join, ctx->aux), "hipEventRecord(join)");
+    uint32_t *point_list = nullptr;
+    if (replay) {
+        GSR_HIP(hipGraphLaunch(e->bin, s), "hipGraphLaunch(binning)");
+        point_list = e->point_list;
+    } else {
+        GSR_TRY(chain_bin(ctx, g, s, &point_list));
+    }
     GSR_HIP(hipStreamWaitEvent(s, ctx->join, 0), "hipStreamWaitEvent(join)");
     GSR_TRY(stage_end(ctx, f, 5));
-    f.point_list = e->point_list;
+    f.point_list = point_list;
     f.tiles_local = nullptr;
     f.id_mask = f.col_shift < 32 ? (1u << f.col_shift) - 1u : 0xFFFFFFFFu;
     GSR_TRY(launch_blend(ctx, f, st, out));
@@ -1088,7 +1123,6 @@ int gsr_create(gsr_context **out) {
     }
     bool ok = hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking, prio_least) ==
                   hipSuccess &&
-              hipStreamCreateWithFlags(&ctx->cap_stream, hipStreamNonBlocking) == hipSuccess &&
               hipMalloc(&ctx->frame_words.p, 64) == hipSuccess &&
               hipMemset(ctx->frame_words.p, 0, 64) == hipSuccess &&
               // stream-to-stream hand-offs on one device: a device-scope release suffices
@@ -1137,7 +1171,6 @@ void gsr_destroy(gsr_context *ctx) {
     if (ctx->join) (void)hipEventDestroy(ctx->join);
     if (ctx->compacted) (void)hipEventDestroy(ctx->compacted);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
-    if (ctx->cap_stream) (void)hipStreamDestroy(ctx->cap_stream);
     if (ctx->h_total) (void)hipHostFree(ctx->h_total);
     delete ctx;
 }
@@ -1161,7 +1194,10 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
             ctx->fast = (int)value;
             return GSR_OK;
         case GSR_OPT_TIGHT_BINNING: ctx->tight = value ? 1 : 0; return GSR_OK;
-        case GSR_OPT_FRAME_GRAPHS: ctx->graphs = value ? 1 : 0; return GSR_OK;
+        case GSR_OPT_FRAME_GRAPHS:
+            if (value < 0 || value > 2) return fail(GSR_E_INVALID, "gsr_set_option: graphs 0..2");
+            ctx->graphs = (int)value;
+            return GSR_OK;
         case GSR_OPT_DEPTH_SORT:
             if (value < -1 || value > 3)
                 return fail(GSR_E_INVALID, "gsr_set_option: depth sort -1..3");

@@ -223,14 +223,16 @@ const char *gsr_stage_name(int i);
  *     after the compaction.  auto = the compaction on strips (a proper subset of the tile rows)
  *     of >= 4M Gaussians, the MSD form when the previous frame's kept keys differed in <= 24
  *     bits (3 or 2), else the LSD passes (1 or 0).  Every form gives the same permutation.
- *   GSR_OPT_FRAME_GRAPHS (default 0): the chains of the frame after the preprocess (the frame
- *     stream's: K, depth sort, binning; the second stream's: tile ranges, blend order, colour)
- *     are recorded once per context and key (input pointers, sizes, strip, workspace) as two
- *     linear HIP graphs and replayed, the binning sized by a capacity (the list lengths seen
- *     so far + 25 %) instead of a mid-frame wait for K; a frame whose list outgrows it is
- *     rendered again the direct way after the capacity grows.  Used for column-first frames
- *     without debug, per-stage timing (gsr_set_timing 1), the compacting depth sort or the rgb
- *     output; the image and every output are the same as with 0.
+ *   GSR_OPT_FRAME_GRAPHS (default 0): deferred-K frames.  1: the chains of the frame after the
+ *     preprocess (the frame stream's K publish + depth sort and its binning; the second
+ *     stream's tile ranges, blend order and colour) are recorded once per context and key
+ *     (input pointers, sizes, strip, workspace) as three linear HIP graphs and replayed; 2: the
+ *     same chains launched directly.  Either way the binning is sized by a capacity (the list
+ *     lengths seen so far + 25 %) instead of a mid-frame wait for K, the host reads K after
+ *     queueing the whole frame, and a frame whose list outgrew the capacity is rendered again
+ *     the direct way after the capacity grows.  Used for column-first frames without debug,
+ *     per-stage timing (gsr_set_timing 1), the compacting depth sort or the rgb output; the
+ *     image and every output are the same as with 0 (DESIGN.md decision 12 has the timings).
  *   GSR_OPT_TIGHT_BINNING (default 1): with the column-first form and no n_contrib output, each
  *     Gaussian of a rect up to 8 tile columns x 15 rows is paired only with the tiles its
  *     alpha >= 1/255 ellipse reaches (upstream's blend skips it on the others), so the lists are

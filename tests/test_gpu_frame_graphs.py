@@ -21,11 +21,12 @@ pytestmark = pytest.mark.gpu
 _next_slot = [20]
 
 
-def _slots(dev):
-    """A fresh (graphs on, graphs off) pair of context slots."""
+def _slots(dev, mode=1):
+    """A fresh (graphs on, graphs off) pair of context slots; mode 1 replays recorded graphs, 2
+    launches the same deferred-K chains directly."""
     on, off = _next_slot[0], _next_slot[0] + 1
     _next_slot[0] += 2
-    set_option(dev, _lib.GSR_OPT_FRAME_GRAPHS, 1, on)
+    set_option(dev, _lib.GSR_OPT_FRAME_GRAPHS, mode, on)
     set_option(dev, _lib.GSR_OPT_FRAME_GRAPHS, 0, off)
     return on, off
 
@@ -74,12 +75,13 @@ CASES = {
 }
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("case", sorted(CASES))
-def test_graph_frames_equal_direct(gpu, case):
+def test_graph_frames_equal_direct(gpu, case, mode):
     build, W, H, tile_rows, radii = CASES[case]
     g, deg = build()
     sc = _scene(gpu, g, deg)
-    on, off = _slots(gpu)
+    on, off = _slots(gpu, mode)
     n = 8
     for cam in _cams(gpu, W, H, n):
         a = _render(gpu, sc, cam, W, H, on, tile_rows, radii)
@@ -108,13 +110,14 @@ def test_graph_frames_precomputed_colours(gpu):
     assert _lib.frame_graph_stats(0, on)["graph_frames"] >= 3
 
 
-def test_graph_overflow_rerenders(gpu):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_graph_overflow_rerenders(gpu, mode):
     """A small scene sets the capacity; a much larger one on the same context overflows it on
     its first frame (rendered again the direct way, identical), then runs on graphs again."""
     W, H = 640, 480
     small = _scene(gpu, synthetic_gaussians(5_000, 3, 31), 3)
     big = _scene(gpu, synthetic_gaussians(150_000, 3, 32), 3)
-    on, off = _slots(gpu)
+    on, off = _slots(gpu, mode)
     cams = _cams(gpu, W, H, 6)
     for cam in cams[:3]:
         _render(gpu, small, cam, W, H, on)
