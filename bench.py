@@ -424,6 +424,10 @@ def main():
             {"auto": -1, "lsd": 0, "compact": 1, "msd": 2, "compact-msd": 3}[args.depth_sort])
         if args.graphs is not None:
             opt(_lib.GSR_OPT_FRAME_GRAPHS, args.graphs)
+    # frame graphs: the pipeline's choice (FramePipeline: on with frames in flight) unless
+    # --graphs; the serial pass below renders as a caller without the pipeline does (direct)
+    graphs_inflight = args.graphs if args.graphs is not None else int(pipe.graphs)
+    graphs_serial = args.graphs if args.graphs is not None else 0
 
     # The untimed diagnostic passes run first, so the device has been rendering for ~200 frames
     # when the timed region starts: a run of 20 timed frames after 5 warmup frames measured
@@ -451,6 +455,7 @@ def main():
 
     # (2) Serial frame rate: one frame in flight (slot 0, the caller's stream, no gather) -- the
     # frame time of a viewer that renders each frame before starting the next.
+    _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_FRAME_GRAPHS, graphs_serial), "gsr_set_option")
     torch.cuda.synchronize()
     n_serial = 100
     t1 = time.perf_counter()
@@ -469,6 +474,7 @@ def main():
     _lib.check(lib.gsr_stage_times(ctx, buf, len(names)), "gsr_stage_times")
     _lib.check(lib.gsr_set_timing(ctx, 0), "gsr_set_timing")
     stage_ms = {n: float(buf[i]) for i, n in enumerate(names)}
+    _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_FRAME_GRAPHS, graphs_inflight), "gsr_set_option")
 
     # Warmup: W frames of the timed loop's own kind (in flight, gathered).
     for i in range(args.warmup):
@@ -586,7 +592,12 @@ def main():
                           "rebalances": len(balancer.history),
                           "note": "cost-weighted strips (StripBalancer): every 8 frames the "
                                   "ranks all-reduce their tile rows' pair counts and re-split"}),
-        "frame_graphs": {f"slot{c}": _lib.frame_graph_stats(local, c) for c in range(args.inflight)},
+        "frame_graphs": {"timed_frames": graphs_inflight, "serial_pass": graphs_serial,
+                         **{f"slot{c}": _lib.frame_graph_stats(local, c)
+                            for c in range(args.inflight)},
+                         "note": "GSR_OPT_FRAME_GRAPHS of the in-flight frames (FramePipeline turns "
+                                 "recorded graphs on when frames overlap) and of the serial pass "
+                                 "(direct launches, as a caller without the pipeline)"},
         "serial_ms_per_frame": round(serial_ms, 4),
         "serial_note": "one frame in flight at a time (no FramePipeline overlap), this rank",
         "roofline": roofline,

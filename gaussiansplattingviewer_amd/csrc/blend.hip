@@ -105,19 +105,28 @@ __device__ __forceinline__ uint32_t order_key(const uint2 *ranges, uint32_t g, u
     return (uint32_t)(kOrderBuckets - 1 - min(k, kOrderBuckets - 1));
 }
 
-__global__ __launch_bounds__(1024) void k_blend_order(const uint2 *__restrict__ ranges,
-                                                      uint32_t n_tiles, uint32_t n_groups,
-                                                      uint32_t *__restrict__ order) {
+#ifndef GSR_ORDER_THREADS
+#define GSR_ORDER_THREADS 1024
+#endif
+constexpr int kOrderThreads = GSR_ORDER_THREADS;  // one block; kOrderBuckets / it per thread
+constexpr int kOrderPer = kOrderBuckets / kOrderThreads;
+__global__ __launch_bounds__(kOrderThreads) void k_blend_order(const uint2 *__restrict__ ranges,
+                                                               uint32_t n_tiles, uint32_t n_groups,
+                                                               uint32_t *__restrict__ order) {
+    GSR_CHAIN_ENTRY();
     __shared__ uint32_t s_h[kOrderBuckets];
-    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_w[kOrderThreads / 64];
     const int tid = threadIdx.x;
-    s_h[tid] = 0u;
+    for (int i = tid; i < kOrderBuckets; i += kOrderThreads) s_h[i] = 0u;
     __syncthreads();
-    for (uint32_t g = tid; g < n_groups; g += 1024) atomicAdd(&s_h[order_key(ranges, g, n_tiles)], 1u);
+    for (uint32_t g = tid; g < n_groups; g += kOrderThreads)
+        atomicAdd(&s_h[order_key(ranges, g, n_tiles)], 1u);
     __syncthreads();
-    // exclusive scan of the 1024 bucket counts
-    const uint32_t c = s_h[tid];
-    uint32_t x = c;
+    // exclusive scan of the 1024 bucket counts, kOrderPer consecutive buckets per thread
+    uint32_t c[kOrderPer], sum = 0;
+#pragma unroll
+    for (int i = 0; i < kOrderPer; ++i) sum += (c[i] = s_h[tid * kOrderPer + i]);
+    uint32_t x = sum;
     const int lane = tid & 63, w = tid >> 6;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -126,11 +135,15 @@ __global__ __launch_bounds__(1024) void k_blend_order(const uint2 *__restrict__ 
     }
     if (lane == 63) s_w[w] = x;
     __syncthreads();
-    uint32_t base = 0;
+    uint32_t base = x - sum;
     for (int i = 0; i < w; ++i) base += s_w[i];
-    s_h[tid] = base + x - c;
+#pragma unroll
+    for (int i = 0; i < kOrderPer; ++i) {
+        s_h[tid * kOrderPer + i] = base;
+        base += c[i];
+    }
     __syncthreads();
-    for (uint32_t g = tid; g < n_groups; g += 1024)
+    for (uint32_t g = tid; g < n_groups; g += kOrderThreads)
         order[atomicAdd(&s_h[order_key(ranges, g, n_tiles)], 1u)] = g;
 }
 
@@ -365,7 +378,7 @@ uint32_t gsr_blend_order_groups(uint32_t n_tiles) {
 hipError_t gsr_launch_blend_order(const uint2 *ranges, uint32_t n_tiles, uint32_t *order,
                                   hipStream_t s) {
     if (n_tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_blend_order, dim3(1), dim3(1024), 0, s, ranges, n_tiles,
+    hipLaunchKernelGGL(k_blend_order, dim3(1), dim3(kOrderThreads), 0, s, ranges, n_tiles,
                        gsr_blend_order_groups(n_tiles), order);
     return hipGetLastError();
 }

@@ -66,6 +66,7 @@ __global__ __launch_bounds__(kDThreads) void k_ds_upsweep(const void *__restrict
                                                           uint32_t *__restrict__ hist,
                                                           const uint32_t *__restrict__ d_n,
                                                           int msd) {
+    GSR_CHAIN_ENTRY();
     __shared__ uint32_t s_h[kDBins];
     __shared__ uint32_t s_red[3][kDW];
     if (kFirst && msd) shift = (int)ctl[2];
@@ -164,6 +165,7 @@ __global__ __launch_bounds__(256) void k_ds_scan(uint32_t *__restrict__ hist, in
                                                  const uint32_t *__restrict__ d_n,
                                                  unsigned long long *host_D, uint32_t tag,
                                                  int msd) {
+    GSR_CHAIN_ENTRY();
     __shared__ uint32_t s_sum[kScanGroups][kScanDigits];
     __shared__ uint32_t s_red[3][4];
     if (kFirst && msd) shift = (int)ctl[2];
@@ -331,6 +333,7 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
     int64_t n_host, int drop, const uint32_t *__restrict__ ctl, int shift,
     const uint32_t *__restrict__ hist, const uint32_t *__restrict__ digit_total,
     const uint32_t *__restrict__ ids_in, const uint32_t *__restrict__ d_n, int msd) {
+    GSR_CHAIN_ENTRY();
     __shared__ uint32_t s_keys[kDT], s_vals[kDT], s_tab[kDBins];  // 48 KiB
     __shared__ uint32_t s_wcnt[kDSubBins * kDW];
     __shared__ uint32_t s_tmp[kDW];
@@ -773,6 +776,7 @@ __global__ __launch_bounds__(kDThreads) void k_ds_local(uint2 *__restrict__ pair
                                                         uint32_t *__restrict__ perm,
                                                         const uint32_t *__restrict__ ctl,
                                                         const uint32_t *__restrict__ digit_total) {
+    GSR_CHAIN_ENTRY();
     __shared__ LocalSmem sm;
     // the bits below the MSD digit: the MSD pass's own shift (ctl[2]); 0 when D <= 12
     const int low = (int)ctl[2];

@@ -15,6 +15,15 @@
 #define GSR_TILE_Y 16
 #define GSR_WAVE 64
 
+// Issue priority of the frame chain's waves (lab switch: build with -DGSR_CHAIN_PRIO=p, 1..3):
+// s_setprio at the entry of every kernel before the blend, so that where two frames are in
+// flight the next frame's chain waves issue ahead of the current frame's blend waves on a SIMD.
+#ifdef GSR_CHAIN_PRIO
+#define GSR_CHAIN_ENTRY() __builtin_amdgcn_s_setprio(GSR_CHAIN_PRIO)
+#else
+#define GSR_CHAIN_ENTRY() ((void)0)
+#endif
+
 namespace gsr {
 
 // One visible Gaussian as the blend consumes it: 48 B, three 16-B loads, gathered by tile

@@ -421,6 +421,7 @@ struct SkipSmem {
 // (A separate pass re-reading the rects and keys took 7 us at C3 and 42 us on a C4 strip.)
 template <bool kSkip>
 __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
+    GSR_CHAIN_ENTRY();
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t key = 0xFFFFFFFFu;
     uint32_t pairs = 0u, tight = 0u;
@@ -514,24 +515,29 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
 // memory (system scope) so the host can read them as soon as this kernel's completion event
 // fires -- no copy, and nothing added to the main stream.  host_K[0] = K, host_K[1] = D,
 // host_K[3] = the pair count over the spans (the high halves of the block counts).
-__global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__restrict__ cnt,
-                                                    const uint2 *__restrict__ keybits, int64_t n,
-                                                    unsigned long long *host_K,
-                                                    uint32_t k_tag, uint32_t *ds_ctl,
-                                                    const uint32_t *d_tag) {
-    __shared__ unsigned long long s_w[16], s_wt[16];
-    __shared__ uint32_t s_or[16], s_and[16];
+#ifndef GSR_PUBLISH_THREADS
+#define GSR_PUBLISH_THREADS 1024
+#endif
+constexpr int kPubThreads = GSR_PUBLISH_THREADS, kPubWaves = kPubThreads / 64;
+__global__ __launch_bounds__(kPubThreads) void k_publish_K(const unsigned long long *__restrict__ cnt,
+                                                           const uint2 *__restrict__ keybits,
+                                                           int64_t n, unsigned long long *host_K,
+                                                           uint32_t k_tag, uint32_t *ds_ctl,
+                                                           const uint32_t *d_tag) {
+    GSR_CHAIN_ENTRY();
+    __shared__ unsigned long long s_w[kPubWaves], s_wt[kPubWaves];
+    __shared__ uint32_t s_or[kPubWaves], s_and[kPubWaves];
     unsigned long long v = 0, vt = 0;
     uint32_t o = 0u, a = 0xFFFFFFFFu;
     // 8 blocks' entries per thread and round, their loads in flight together (one dependent
     // load per 1024 blocks took 23 us at 6M Gaussians)
     constexpr int kU = 8;
-    for (int64_t i0 = threadIdx.x; i0 < n; i0 += kU * 1024) {
+    for (int64_t i0 = threadIdx.x; i0 < n; i0 += kU * kPubThreads) {
         unsigned long long c[kU];
         uint2 kb[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            const int64_t i = i0 + (int64_t)u * 1024;
+            const int64_t i = i0 + (int64_t)u * kPubThreads;
             c[u] = i < n ? cnt[i] : 0ull;
             kb[u] = i < n ? keybits[i] : make_uint2(0u, 0xFFFFFFFFu);
         }
@@ -561,7 +567,7 @@ __global__ __launch_bounds__(1024) void k_publish_K(const unsigned long long *__
         unsigned long long t = 0, tt = 0;
         o = 0u;
         a = 0xFFFFFFFFu;
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < kPubWaves; ++i) {
             t += s_w[i];
             tt += s_wt[i];
             o |= s_or[i];
@@ -642,6 +648,7 @@ __device__ __forceinline__ void store_color(const GsrPreprocessArgs &a, int64_t 
 // through an LDS slab (every line moves L2 -> L1 once, but all 64 rows are read where ~60 % are
 // needed: 3,259 vs 3,400 frames/s); an LDS transpose of all 64 rows at once (144 vs 83 us).
 __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
+    GSR_CHAIN_ENTRY();
     extern __shared__ uint32_t s_occupancy_cap[];  // reserved only to cap blocks per CU
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t n_waves = (a.P + 63) / 64;
@@ -760,7 +767,7 @@ hipError_t gsr_launch_count_pairs(const GsrPreprocessArgs &a, hipStream_t s, uin
     if (a.P == 0) return hipSuccess;
     const unsigned g = grid_for(a.P);  // the preprocess's blocks
     const uint2 *keybits = reinterpret_cast<const uint2 *>(a.block_pairs + g);
-    hipLaunchKernelGGL(k_publish_K, dim3(1), dim3(1024), 0, s,
+    hipLaunchKernelGGL(k_publish_K, dim3(1), dim3(kPubThreads), 0, s,
                        reinterpret_cast<const unsigned long long *>(a.block_pairs), keybits,
                        (int64_t)g, a.host_K, d_tag ? 0u : a.k_tag, ds_ctl, d_tag);
     return hipGetLastError();
