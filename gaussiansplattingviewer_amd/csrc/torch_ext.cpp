@@ -74,8 +74,11 @@ rasterize_gaussians(const torch::Tensor &background, const torch::Tensor &means3
     const int64_t P = means3D.size(0);
     const int64_t H = image_height, W = image_width;
     auto f32 = means3D.options().dtype(torch::kFloat32);
-    torch::Tensor color = torch::full({3, H, W}, 0.0, f32);
-    torch::Tensor radii = torch::full({P}, 0, means3D.options().dtype(torch::kInt32));
+    // upstream zero-fills both; the forward writes every pixel and every radius (P > 0), so
+    // only an empty scene needs the fill (two fill kernels fewer per frame)
+    torch::Tensor color = P ? torch::empty({3, H, W}, f32) : torch::zeros({3, H, W}, f32);
+    torch::Tensor radii = P ? torch::empty({P}, means3D.options().dtype(torch::kInt32))
+                            : torch::zeros({P}, means3D.options().dtype(torch::kInt32));
     auto bytes = means3D.options().dtype(torch::kUInt8);
     torch::Tensor geom = torch::empty({0}, bytes), binning = torch::empty({0}, bytes),
                   img = torch::empty({0}, bytes);
@@ -113,7 +116,11 @@ rasterize_gaussians(const torch::Tensor &background, const torch::Tensor &means3
         c10::hip::HIPGuard guard(dev.index());
         gsr_context *ctx = context_for(dev.index());
         hipStream_t s = c10::hip::getCurrentHIPStream(dev.index()).stream();
-        const int rc = gsr_forward(ctx, &g, &st, &out, s);
+        int rc;
+        {  // the forward waits for K (pinned memory): other Python threads may run meanwhile
+            pybind11::gil_scoped_release no_gil;
+            rc = gsr_forward(ctx, &g, &st, &out, s);
+        }
         TORCH_CHECK(rc == GSR_OK, "gsr_forward failed (", rc, "): ", gsr_last_error());
         num_rendered = out.num_rendered;
     }
