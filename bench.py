@@ -387,7 +387,10 @@ def main():
     balancer = StripBalancer(gy, gx, world, rank, device=dev) if world > 1 else None
     # frames in flight: frame i renders on stream i % D with context slot i % D, so the next
     # frame's latency-bound preprocess / sort / binning overlap this frame's blend
-    pipe = FramePipeline(args.inflight, dev)
+    # strip frames (a rank of an N-GPU frame, or the simulated strip) replay frame graphs: with
+    # two in flight a strip rank's rate is then steady instead of bimodal run to run (DESIGN.md
+    # decision 12); full frames keep direct launches
+    pipe = FramePipeline(args.inflight, dev, graphs=args.inflight >= 2 and (world > 1 or bool(args.sim_strip)))
 
     def step(i):
         with pipe.frame() as slot:
@@ -424,8 +427,8 @@ def main():
             {"auto": -1, "lsd": 0, "compact": 1, "msd": 2, "compact-msd": 3}[args.depth_sort])
         if args.graphs is not None:
             opt(_lib.GSR_OPT_FRAME_GRAPHS, args.graphs)
-    # frame graphs: the pipeline's choice (FramePipeline: on with frames in flight) unless
-    # --graphs; the serial pass below renders as a caller without the pipeline does (direct)
+    # frame graphs: the pipeline's choice (strip frames in flight) unless --graphs; the serial
+    # pass below renders as a caller without the pipeline does (direct launches)
     graphs_inflight = args.graphs if args.graphs is not None else int(pipe.graphs)
     graphs_serial = args.graphs if args.graphs is not None else 0
 
@@ -595,9 +598,9 @@ def main():
         "frame_graphs": {"timed_frames": graphs_inflight, "serial_pass": graphs_serial,
                          **{f"slot{c}": _lib.frame_graph_stats(local, c)
                             for c in range(args.inflight)},
-                         "note": "GSR_OPT_FRAME_GRAPHS of the in-flight frames (FramePipeline turns "
-                                 "recorded graphs on when frames overlap) and of the serial pass "
-                                 "(direct launches, as a caller without the pipeline)"},
+                         "note": "GSR_OPT_FRAME_GRAPHS of the in-flight frames (recorded graphs "
+                                 "for strip frames, direct launches for full frames) and of the "
+                                 "serial pass (direct launches, as a caller without the pipeline)"},
         "serial_ms_per_frame": round(serial_ms, 4),
         "serial_note": "one frame in flight at a time (no FramePipeline overlap), this rank",
         "roofline": roofline,

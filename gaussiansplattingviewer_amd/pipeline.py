@@ -32,7 +32,7 @@ class FramePipeline:
     (`wait(stream_of_frame)`); `torch.cuda.synchronize()` waits for all of them.
     """
 
-    def __init__(self, depth: int = 2, device=None, graphs: bool | None = None):
+    def __init__(self, depth: int = 2, device=None, graphs: bool = False):
         if depth < 1:
             raise ValueError("depth must be >= 1")
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
@@ -41,14 +41,15 @@ class FramePipeline:
         self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                             for _ in range(depth - 1)]
         self.count = 0
-        # Frame graphs (gsr.h GSR_OPT_FRAME_GRAPHS 1) on the slots' contexts when frames overlap
-        # (depth >= 2, unless graphs=False): the host queues a frame in a few graph launches
-        # and reads K after the whole frame is queued, so it keeps ahead of the overlapping
-        # frames (C3 in flight +1.4 %, C3 strips 8.5-10.8k -> 10.5k frames/s, the P=2000 host
-        # loop 86 -> 63 us per frame; profiles/r05l_ab_frame_graphs.txt).  A serial frame pays
-        # ~15 us of GPU time for them (graph dispatch), so depth 1 keeps the direct launches.
-        # The images are bit-identical either way (tests/test_gpu_frame_graphs.py).
-        self.graphs = (depth >= 2) if graphs is None else bool(graphs)
+        # graphs=True: frame graphs (gsr.h GSR_OPT_FRAME_GRAPHS 1) on the slots' contexts; the
+        # host queues a frame in a few graph launches and reads K after the whole frame is
+        # queued.  With two frames in flight that pays on strip frames (a C3 3/8 strip 8.5-10.8k
+        # frames/s run to run -> a steady 10.5k, the multi-GPU ranks' regime) and on a tiny scene
+        # (the P=2000 host loop 86 -> 63 us), but not on full frames (C3 +1.4 %, C5 and c3r
+        # -2 %, C4 even; profiles/r05l_ab_frame_graphs.txt, r05o_ab_graphs_configs.txt), and a
+        # serial frame pays ~15 us of GPU time for graph dispatch.  Images are bit-identical
+        # either way (tests/test_gpu_frame_graphs.py).
+        self.graphs = bool(graphs)
         from . import _lib
         index = dev.index if dev.index is not None else torch.cuda.current_device()
         for slot in range(depth):

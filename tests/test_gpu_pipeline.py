@@ -35,8 +35,10 @@ def _render(dg, cam, W, H, dev, slot=0, tile_rows=None):
         False, False, slot=slot, tile_rows=tile_rows)
 
 
-@pytest.mark.parametrize("depth,tile_rows", [(2, None), (3, None), (2, (3, 9))])
-def test_pipelined_frames_equal_serial(gpu, depth, tile_rows):
+@pytest.mark.parametrize("depth,tile_rows,graphs", [(2, None, False), (3, None, False),
+                                                    (2, (3, 9), False), (2, None, True),
+                                                    (2, (3, 9), True)])
+def test_pipelined_frames_equal_serial(gpu, depth, tile_rows, graphs):
     P, W, H, n = 60_000, 640, 480, 9
     _, dg, cams = _scene(gpu, P, W, H, n, seed=11)
     serial = []
@@ -45,13 +47,14 @@ def test_pipelined_frames_equal_serial(gpu, depth, tile_rows):
         serial.append((r.num_rendered, r.color.clone(), r.radii.clone()))
     torch.cuda.synchronize()
 
-    pipe = FramePipeline(depth, gpu)
+    pipe = FramePipeline(depth, gpu, graphs=graphs)  # (frame graphs: GSR_OPT_FRAME_GRAPHS 1)
     piped = []
     for cam in cams:
         with pipe.frame() as slot:
             r = _render(dg, cam, W, H, gpu, slot=slot, tile_rows=tile_rows)
             piped.append((r.num_rendered, r.color, r.radii))
     torch.cuda.synchronize()
+    FramePipeline(depth, gpu, graphs=False)  # (later tests see direct launches again)
     for (k0, c0, r0), (k1, c1, r1) in zip(serial, piped):
         assert k0 == k1
         assert torch.equal(r0, r1)
