@@ -65,16 +65,21 @@ constexpr int kTimingRing = 256;  // frames whose stage events are kept
 // stores (k_publish_K, the depth sort's pass 0); after this long without them it falls back to a
 // blocking wait (K) or queues every depth pass (D).
 constexpr auto kSpinLimit = std::chrono::milliseconds(50);
-// Frames with at least this many pairs wait for D before queueing the depth sort's later passes
-// (an empty third pass stays off the GPU: C3 3,480 vs 3,340 frames/s); smaller frames are bound
-// by the host's submission rate, which the wait would hold to the GPU (DESIGN.md §3 decision 2).
+// Frames with at least this many pairs wait for D before queueing the LSD depth sort's later
+// passes (an empty third pass stays off the GPU: C3 3,480 vs 3,340 frames/s); smaller frames are
+// bound by the host's submission rate, which the wait would hold to the GPU (DESIGN.md §3
+// decision 2).  Only while the previous frame's D left a pass to skip (<= 24 bits): a frame whose
+// keys vary in more bits needs all three, and the wait only holds the host (c3r, D = 31).
 constexpr int64_t kWaitDPairs = 4 << 20;
 // The depth sort compacts the kept keys first on strips of at least this many Gaussians
 // (GSR_OPT_DEPTH_SORT auto): a 1/8 strip of C4 keeps ~1/8 of them (DESIGN.md decision 2).
 constexpr int64_t kCompactP = 4 << 20;
-// The MSD depth sort for frames whose previous frame's kept depth keys differed in <= this many
-// bits (setup_frame).
-constexpr uint32_t kMsdMaxD = 24;
+// The MSD depth sort for frames whose previous frame's kept depth keys spanned a range of <= this
+// many bits (setup_frame; lab builds override it with -DGSR_MSD_MAX_D).
+#ifndef GSR_MSD_MAX_D
+#define GSR_MSD_MAX_D 25
+#endif
+constexpr uint32_t kMsdMaxD = GSR_MSD_MAX_D;
 
 const char *kStageNames[kAllStages] = {"preprocess", "depth_sort", "scan",  "duplicate",
                                        "tile_sort",  "ranges",     "blend", "color"};
@@ -128,15 +133,16 @@ struct gsr_context {
     DevBuf tile_diff;  // difference-array partials of the second-stream tile ranges
     DevBuf blend_order;  // the blend's tile groups, heaviest first (second stream)
     // pinned host words the GPU stores into: [0] -, [1] -, [2] K (k_publish_K), [3] its depth-key
-    // bits, [4] (frame tag << 32) | D from the depth sort's pass 0, [5] the pair count over the
-    // spans (k_publish_K), [6] -, [7] K's tag
+    // bits D, [4] (frame tag << 32) | D from the depth sort's pass 0, [5] the pair count over the
+    // spans (k_publish_K), [6] the bits of the kept depth keys' range (k_publish_K), [7] K's tag
     uint64_t *h_total = nullptr;
     unsigned long long *d_hostK = nullptr;  // device view of h_total + 2
     unsigned long long *d_hostD = nullptr;  // device view of h_total + 4
     uint32_t sort_tag = 0;                  // frames rendered on this context (the pinned tags)
-    // key bits of the last frame's kept depths (wait_K); the first frame, with no history,
-    // takes the LSD sort, which any spread of depths suits (the MSD form wants D <= 24)
-    uint32_t last_D = UINT32_MAX;
+    // the bits of the last frame's kept depth keys' range and the bits in which they differ
+    // (wait_K); the first frame, with no history, takes the LSD sort, which any spread of depths
+    // suits
+    uint32_t last_Dr = UINT32_MAX, last_D = UINT32_MAX;
     // state of the last forward (gsr_get_binning, gsr_tile_row_pairs)
     bool have_forward = false;
     int64_t last_K = 0;        // upstream's num_rendered
@@ -416,12 +422,14 @@ int setup_frame(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     f.compact_sort = ctx->depth_sort < 0 ? (f.rows_tiles < f.gy && P >= kCompactP)
                                          : ctx->depth_sort == 1 || ctx->depth_sort == 3;
     pa.block_kept = f.compact_sort ? static_cast<uint32_t *>(ctx->block_kept.p) : nullptr;
-    // the MSD sort wants buckets of a few thousand keys: its 4096 buckets split the top 12 of the
-    // D varying key bits, which balances them when D <= 24 (depths within one or two float
-    // exponents, C2-C5).  Wider spreads (the clustered c3r, D = 31) crowd some buckets past the
-    // LDS sort, so they keep the LSD passes; the choice follows the previous frame's D (the
-    // result is the same either way, only the time differs)
-    f.msd_sort = ctx->depth_sort < 0 ? ctx->last_D <= (uint32_t)kMsdMaxD
+    // the MSD sort wants buckets of a few thousand keys: its 4096 buckets split the top 12 bits of
+    // the kept keys' range (key - min), which balances them while the depths span a few float
+    // exponents (Dr <= 25: C2, C3, C5 -- whose near Gaussians cross depth 2.0, D = 31 but Dr =
+    // 24-25; C5 in flight +4 %, profiles/r05q_ab_range_msd.txt); wider ranges crowd some buckets
+    // past the LDS sort (c3r, Dr = 26: serial 0.313 -> 0.340 ms), so they keep the LSD passes.
+    // The choice follows the previous frame's range (the result is the same either way, only the
+    // time differs)
+    f.msd_sort = ctx->depth_sort < 0 ? ctx->last_Dr <= (uint32_t)kMsdMaxD
                                      : ctx->depth_sort >= 2;
     // (compacted strips keep the second stream's publish: on the C4 1/8 strip the main-stream
     // publish let the tile counts and colour start earlier, beside the depth sort, 80 -> 134 us)
@@ -583,6 +591,7 @@ int wait_K(gsr_context *ctx, Frame &f) {
         GSR_HIP(hipStreamSynchronize(f.main_publish ? f.s : ctx->aux),
                 "hipStreamSynchronize(pair count)");
     f.K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
+    ctx->last_Dr = (uint32_t)__atomic_load_n(&ctx->h_total[6], __ATOMIC_ACQUIRE);
     ctx->last_D = (uint32_t)__atomic_load_n(&ctx->h_total[3], __ATOMIC_ACQUIRE);
     f.KL = f.tight ? __atomic_load_n(&ctx->h_total[5], __ATOMIC_ACQUIRE) : f.K;
     if (f.dbg) {
@@ -988,6 +997,7 @@ int forward_graph(gsr_context *ctx, Frame &f, const gsr_raster_settings *st, gsr
         GSR_HIP(hipStreamSynchronize(f.main_publish ? s : ctx->aux),
                 "hipStreamSynchronize(pair count)");
     f.K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
+    ctx->last_Dr = (uint32_t)__atomic_load_n(&ctx->h_total[6], __ATOMIC_ACQUIRE);
     ctx->last_D = (uint32_t)__atomic_load_n(&ctx->h_total[3], __ATOMIC_ACQUIRE);
     f.KL = f.tight ? __atomic_load_n(&ctx->h_total[5], __ATOMIC_ACQUIRE) : f.K;
     if (f.K > (uint64_t)UINT32_MAX - 4096)
@@ -1057,7 +1067,7 @@ int forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings 
     if (!f.msd_sort) {  // the LSD sort: the passes D needs
         int depth_passes = gsr_depth_sort_passes(32);  // all
         uint64_t dv = 0;
-        if (ctx->last_K >= kWaitDPairs &&
+        if (ctx->last_K >= kWaitDPairs && ctx->last_D <= 2u * 12u &&
             spin_on(&ctx->h_total[4], [&](uint64_t v) { return (uint32_t)(v >> 32) == f.tag; },
                     dv))
             depth_passes = gsr_depth_sort_passes((uint32_t)dv);

@@ -47,11 +47,18 @@ static_assert(kDSubBins * kDW == kDThreads, "one thread per (sub-digit, wave) in
 constexpr int kDPer = kDBins / kDThreads;  // digit starts per thread in the prologue
 static_assert(kDPer == 8, "two 16-B loads of digit totals and of the hist row per thread");
 
-// ctl: [0] kept count, [1] D (key bits to sort), [2] the MSD pass's shift (D - 12, or 0 when
-// D <= 12; written by k_ds_bits or gsr_launch_count_pairs before the MSD pass), [3] unused, then
-// per tile uint4 {OR, AND, kept, 0} of pass 0.  The MSD kernels read only ctl[2]: the LSD form's
-// pass-0 scan also rewrites ctl[1] from the sort's own tiles (in the MSD form a diagnostic that
-// debug forwards compare with the preprocess's D, api.hip wait_K).
+// ctl: [0] kept count, [1] D (key bits to sort), [2] the MSD pass's shift and [3] the smallest
+// kept key (gsr_msd_ctl: the MSD pass buckets key - min by its top 12 range bits; written by
+// k_ds_bits or gsr_launch_count_pairs before the MSD pass), then per tile uint4 {OR, AND, kept,
+// 0} of pass 0.  The MSD kernels read only ctl[2] and ctl[3]: the pass-0 scan also rewrites
+// ctl[1] from the sort's own tiles (in the MSD form a diagnostic that debug forwards compare
+// with the preprocess's D, api.hip wait_K).
+//
+// The MSD pass works on key - min (the range-relative key): every kept key is a positive
+// float's bits, so key - min keeps the order, and its bits above the range's are 0.  Bucketing
+// the top 12 of the range's bits, not of the bits that vary, keeps the buckets even where one
+// outlier flips a high bit (a near Gaussian at depth 1.9 among depths in [2, 8): D = 31 but a
+// range of 25 bits).  The pass writes range-relative keys; k_ds_local sorts them by the rest.
 constexpr int kCtlHead = 4;
 
 __device__ __forceinline__ int pass_bits(int shift) { return min(kDBits, 32 - shift); }
@@ -70,6 +77,7 @@ __global__ __launch_bounds__(kDThreads) void k_ds_upsweep(const void *__restrict
     __shared__ uint32_t s_h[kDBins];
     __shared__ uint32_t s_red[3][kDW];
     if (kFirst && msd) shift = (int)ctl[2];
+    const uint32_t kmin = (kFirst && msd) ? ctl[3] : 0u;  // range-relative MSD keys
     int64_t n = d_n ? (int64_t)*d_n : n_host;  // d_n: the compacted count (first pass)
     if (!kFirst) {
         if (ctl[1] <= (uint32_t)shift) return;  // constant digit: pass skipped
@@ -85,7 +93,7 @@ __global__ __launch_bounds__(kDThreads) void k_ds_upsweep(const void *__restrict
     uint32_t vor = 0u, vand = 0xFFFFFFFFu, cnt = 0u;
     auto add = [&](uint32_t k) {
         if (kFirst && drop && k == kDropKey) return;
-        atomicAdd(&s_h[(k >> shift) & mask], 1u);
+        atomicAdd(&s_h[((k - kmin) >> shift) & mask], 1u);
         if (kFirst) {
             vor |= k;
             vand &= k;
@@ -339,6 +347,7 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
     __shared__ uint32_t s_tmp[kDW];
     const uint32_t D = ctl[1];
     if (kFirst && msd) shift = (int)ctl[2];
+    const uint32_t kmin = (kFirst && msd) ? ctl[3] : 0u;  // range-relative MSD keys
     int64_t n = d_n ? (int64_t)*d_n : n_host;
     if (!kFirst) {
         if (D <= (uint32_t)shift) return;
@@ -367,6 +376,7 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
             v[j] = q.y;
         }
         if (valid && !(kFirst && drop && k[j] == kDropKey)) keep |= 1u << j;
+        k[j] -= kmin;  // (MSD: ranked, bucketed and written range-relative)
     }
     // s_tab[d] = start of digit d overall + its count in earlier tiles (8 digits per thread:
     // the exclusive scan of the digit totals plus this tile's row of the scanned histogram)
@@ -516,8 +526,8 @@ __global__ __launch_bounds__(256) void k_ds_compact(const uint32_t *__restrict__
 // 0.2), never 0, so OR == 0 means no kept key (D = 0).
 __global__ __launch_bounds__(1024) void k_ds_bits(const uint2 *__restrict__ keybits, int64_t nb,
                                                   uint32_t *__restrict__ ctl) {
-    __shared__ uint32_t s_or[16], s_and[16];
-    uint32_t o = 0u, a = 0xFFFFFFFFu;
+    __shared__ uint32_t s_max[16], s_min[16];
+    uint32_t mx = 0u, mn = 0xFFFFFFFFu;  // the preprocess blocks' {largest, smallest} kept key
     constexpr int kU = 8;  // loads in flight per thread
     for (int64_t i0 = threadIdx.x; i0 < nb; i0 += kU * 1024) {
         uint2 kb[kU];
@@ -527,22 +537,19 @@ __global__ __launch_bounds__(1024) void k_ds_bits(const uint2 *__restrict__ keyb
             kb[u] = i < nb ? keybits[i] : make_uint2(0u, 0xFFFFFFFFu);
         }
 #pragma unroll
-        for (int u = 0; u < kU; ++u) o |= kb[u].x, a &= kb[u].y;
+        for (int u = 0; u < kU; ++u) mx = max(mx, kb[u].x), mn = min(mn, kb[u].y);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-        o |= __shfl_xor(o, off);
-        a &= __shfl_xor(a, off);
+        mx = max(mx, (uint32_t)__shfl_xor(mx, off));
+        mn = min(mn, (uint32_t)__shfl_xor(mn, off));
     }
-    if ((threadIdx.x & 63) == 0) s_or[threadIdx.x >> 6] = o, s_and[threadIdx.x >> 6] = a;
+    if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = mx, s_min[threadIdx.x >> 6] = mn;
     __syncthreads();
     if (threadIdx.x == 0) {
-        o = 0u, a = 0xFFFFFFFFu;
-        for (int i = 0; i < 16; ++i) o |= s_or[i], a &= s_and[i];
-        const uint32_t diff = o ? (o ^ a) : 0u;
-        const uint32_t D = diff ? 32u - (uint32_t)__clz(diff) : 0u;
-        ctl[1] = D;
-        ctl[2] = D > (uint32_t)kDBits ? D - (uint32_t)kDBits : 0u;
+        mx = 0u, mn = 0xFFFFFFFFu;
+        for (int i = 0; i < 16; ++i) mx = max(mx, s_max[i]), mn = min(mn, s_min[i]);
+        gsr_msd_ctl(key_bits(mx, mn), ctl);
     }
 }
 

@@ -195,6 +195,30 @@ __device__ __forceinline__ void col_span(uint2 rect, uint2 cols, uint32_t c, uin
     }
 }
 
+// --- the depth keys' spread (the preprocess blocks' largest / smallest kept key) -------------
+// D: the bits in which the kept keys differ (the highest bit where the largest and the smallest
+// differ: every key in between shares the bits above it); Dr: the bits of their range
+// max - min, which the MSD depth sort buckets (key - min) by.  No kept key: max < min.
+struct KeyBits {
+    uint32_t D, Dr, min;
+};
+__device__ __forceinline__ KeyBits key_bits(uint32_t mx, uint32_t mn) {
+    KeyBits k{0u, 0u, 0u};
+    if (mx >= mn) {
+        k.D = mx != mn ? 32u - (uint32_t)__clz(mx ^ mn) : 0u;
+        k.Dr = mx != mn ? 32u - (uint32_t)__clz(mx - mn) : 0u;
+        k.min = mn;
+    }
+    return k;
+}
+// The MSD depth sort's control words (depth_sort.hip): ctl[1] = D, ctl[2] = the MSD pass's
+// shift (Dr - 12, or 0: (key - min) >> shift is the 12-bit bucket), ctl[3] = min.
+__device__ __forceinline__ void gsr_msd_ctl(const KeyBits &k, uint32_t *ctl) {
+    ctl[1] = k.D;
+    ctl[2] = k.Dr > 12u ? k.Dr - 12u : 0u;
+    ctl[3] = k.min;
+}
+
 // --- wave / block scans (256-thread blocks, wave64) ------------------------------------
 __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
     const int lane = threadIdx.x & 63;

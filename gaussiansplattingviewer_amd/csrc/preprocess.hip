@@ -475,19 +475,20 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
         }
     }
     const bool kept = pairs != 0u;  // has pairs in the strip <=> its depth key is kept
-    uint32_t v = pairs, o = kept ? key : 0u, an = kept ? key : 0xFFFFFFFFu;  // v <= 256 x 2^16
+    // the block's pair count (v <= 256 x 2^16) and the largest / smallest kept depth key
+    uint32_t v = pairs, mx = kept ? key : 0u, mn = kept ? key : 0xFFFFFFFFu;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         v += __shfl_xor(v, off);
         tight += __shfl_xor(tight, off);
-        o |= __shfl_xor(o, off);
-        an &= __shfl_xor(an, off);
+        mx = max(mx, (uint32_t)__shfl_xor(mx, off));
+        mn = min(mn, (uint32_t)__shfl_xor(mn, off));
     }
     __shared__ uint32_t s_red[5][4];
     const uint32_t c = a.block_kept ? (uint32_t)__popcll(__ballot(kept)) : 0u;
     if ((threadIdx.x & 63) == 0) {
         const int w = threadIdx.x >> 6;
-        s_red[0][w] = v, s_red[1][w] = o, s_red[2][w] = an, s_red[3][w] = c, s_red[4][w] = tight;
+        s_red[0][w] = v, s_red[1][w] = mx, s_red[2][w] = mn, s_red[3][w] = c, s_red[4][w] = tight;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -503,8 +504,8 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
             ((uint64_t)(s_red[4][0] + s_red[4][1] + s_red[4][2] + s_red[4][3]) << 32) |
             (s_red[0][0] + s_red[0][1] + s_red[0][2] + s_red[0][3]);
         reinterpret_cast<uint2 *>(a.block_pairs + gridDim.x)[blockIdx.x] =
-            make_uint2(s_red[1][0] | s_red[1][1] | s_red[1][2] | s_red[1][3],
-                       s_red[2][0] & s_red[2][1] & s_red[2][2] & s_red[2][3]);
+            make_uint2(max(max(s_red[1][0], s_red[1][1]), max(s_red[1][2], s_red[1][3])),
+                       min(min(s_red[2][0], s_red[2][1]), min(s_red[2][2], s_red[2][3])));
         if (a.block_kept) a.block_kept[blockIdx.x] = s_red[3][0] + s_red[3][1] + s_red[3][2] + s_red[3][3];
     }
 }
@@ -526,9 +527,9 @@ __global__ __launch_bounds__(kPubThreads) void k_publish_K(const unsigned long l
                                                            const uint32_t *d_tag) {
     GSR_CHAIN_ENTRY();
     __shared__ unsigned long long s_w[kPubWaves], s_wt[kPubWaves];
-    __shared__ uint32_t s_or[kPubWaves], s_and[kPubWaves];
+    __shared__ uint32_t s_max[kPubWaves], s_min[kPubWaves];
     unsigned long long v = 0, vt = 0;
-    uint32_t o = 0u, a = 0xFFFFFFFFu;
+    uint32_t mx = 0u, mn = 0xFFFFFFFFu;  // the largest / smallest kept depth key
     // 8 blocks' entries per thread and round, their loads in flight together (one dependent
     // load per 1024 blocks took 23 us at 6M Gaussians)
     constexpr int kU = 8;
@@ -545,43 +546,42 @@ __global__ __launch_bounds__(kPubThreads) void k_publish_K(const unsigned long l
         for (int u = 0; u < kU; ++u) {
             v += c[u] & 0xFFFFFFFFull;
             vt += c[u] >> 32;
-            o |= kb[u].x;
-            a &= kb[u].y;
+            mx = max(mx, kb[u].x);
+            mn = min(mn, kb[u].y);
         }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         v += __shfl_xor(v, off);
         vt += __shfl_xor(vt, off);
-        o |= __shfl_xor(o, off);
-        a &= __shfl_xor(a, off);
+        mx = max(mx, (uint32_t)__shfl_xor(mx, off));
+        mn = min(mn, (uint32_t)__shfl_xor(mn, off));
     }
     if ((threadIdx.x & 63) == 0) {
         s_w[threadIdx.x >> 6] = v;
         s_wt[threadIdx.x >> 6] = vt;
-        s_or[threadIdx.x >> 6] = o;
-        s_and[threadIdx.x >> 6] = a;
+        s_max[threadIdx.x >> 6] = mx;
+        s_min[threadIdx.x >> 6] = mn;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long t = 0, tt = 0;
-        o = 0u;
-        a = 0xFFFFFFFFu;
+        mx = 0u;
+        mn = 0xFFFFFFFFu;
         for (int i = 0; i < kPubWaves; ++i) {
             t += s_w[i];
             tt += s_wt[i];
-            o |= s_or[i];
-            a &= s_and[i];
+            mx = max(mx, s_max[i]);
+            mn = min(mn, s_min[i]);
         }
-        const uint32_t diff = t ? (o ^ a) : 0u;
-        const unsigned long long D = diff ? 32u - (uint32_t)__clz(diff) : 0u;
-        if (ds_ctl) {  // the MSD depth sort's D and shift (as k_ds_bits; OR == 0: no kept key)
-            const uint32_t kd = o ? (o ^ a) : 0u;
-            const uint32_t d2 = kd ? 32u - (uint32_t)__clz(kd) : 0u;
-            ds_ctl[1] = d2;
-            ds_ctl[2] = d2 > 12u ? d2 - 12u : 0u;
-        }
-        __hip_atomic_store(host_K + 1, D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // D: the key bits that vary (the highest bit where the smallest and the largest kept key
+        // differ is the highest bit any two kept keys differ in); Dr: the bits of their range
+        const KeyBits kb = key_bits(mx, mn);
+        if (ds_ctl) gsr_msd_ctl(kb, ds_ctl);  // the MSD depth sort's control words
+        __hip_atomic_store(host_K + 1, (unsigned long long)kb.D, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_K + 4, (unsigned long long)kb.Dr, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(host_K + 3, tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(host_K, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         // the host spins on this tag instead of sleeping in an event wait (release: K and D are
