@@ -84,8 +84,8 @@ def parse():
     ap.add_argument("--depth-sort", default="auto", choices=["auto", "lsd", "compact", "msd", "compact-msd"],
                     help="GSR_OPT_DEPTH_SORT: LSD passes, LSD after compacting the kept keys, or "
                          "the MSD pass + per-bucket local sort (auto: compact on strips of >= 4M "
-                         "Gaussians, else MSD when the last frame's depth keys differed in <= 24 "
-                         "bits, else LSD)")
+                         "Gaussians, else MSD when the last frame's kept depth keys spanned a "
+                         "range of <= 25 bits, else LSD)")
     ap.add_argument("--graphs", type=int, default=None, choices=[0, 1, 2],
                     help="GSR_OPT_FRAME_GRAPHS for every context slot (default: the library's): "
                          "0 direct, 1 recorded graphs, 2 the deferred-K chains launched directly")

@@ -218,11 +218,12 @@ const char *gsr_stage_name(int i);
  *     per-pixel operation order (IEEE, no FMA, ocml expf).
  *   GSR_OPT_DEPTH_SORT (default -1 = auto): the form of the per-frame depth sort.  0 = LSD passes
  *     of 12 key bits, the first dropping the keys of Gaussians without pairs in the strip;
- *     1 = the same after a compaction of the kept keys; 2 = one MSD pass over the top 12 of the
- *     bits in which the kept keys differ, then every bucket sorted by the rest in LDS; 3 = 2
- *     after the compaction.  auto = the compaction on strips (a proper subset of the tile rows)
- *     of >= 4M Gaussians, the MSD form when the previous frame's kept keys differed in <= 24
- *     bits (3 or 2), else the LSD passes (1 or 0).  Every form gives the same permutation.
+ *     1 = the same after a compaction of the kept keys; 2 = one MSD pass over the top 12 bits
+ *     of the kept keys' range (key - smallest kept key), then every bucket sorted by the rest in
+ *     LDS; 3 = 2 after the compaction.  auto = the compaction on strips (a proper subset of the
+ *     tile rows) of >= 4M Gaussians, the MSD form when the previous frame's kept keys spanned a
+ *     range of <= 25 bits (3 or 2), else the LSD passes (1 or 0).  Every form gives the same
+ *     permutation.
  *   GSR_OPT_FRAME_GRAPHS (default 0): deferred-K frames.  1: the chains of the frame after the
  *     preprocess (the frame stream's K publish + depth sort and its binning; the second
  *     stream's tile ranges, blend order and colour) are recorded once per context and key
