@@ -16,6 +16,7 @@ run c3 --config c3 --steps 200 --warmup 20 --no-cpu-baseline
 run c5 --config c5 --steps 1000 --warmup 50 --no-cpu-baseline
 run c3r --config c3r --steps 200 --warmup 20 --no-cpu-baseline
 run c3_strip3of8 --config c3 --sim-strip 3/8 --steps 500 --warmup 50 --no-cpu-baseline
+run c3_strip0of8 --config c3 --sim-strip 0/8 --steps 500 --warmup 50 --no-cpu-baseline
 run c4_full --config c4 --steps 50 --warmup 5 --no-cpu-baseline
 for r in 0 1 2 3 4 5 6 7; do
   run c4_strip${r}of8 --config c4 --sim-strip $r/8 --steps 100 --warmup 10 --no-cpu-baseline
