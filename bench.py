@@ -78,9 +78,10 @@ def parse():
     ap.add_argument("--blend", default="fast", choices=["exact", "fast"],
                     help="blend arithmetic: GSR_OPT_BLEND_FAST (default) or upstream's exact "
                          "operation order")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight (FramePipeline: own stream + context slot each); "
-                         "1 = serial forwards")
+                         "1 = serial forwards (default: 4 full frames, each on one stream; 2 "
+                         "strip frames, each with its second stream and frame graphs)")
     ap.add_argument("--depth-sort", default="auto", choices=["auto", "lsd", "compact", "msd", "compact-msd"],
                     help="GSR_OPT_DEPTH_SORT: LSD passes, LSD after compacting the kept keys, or "
                          "the MSD pass + per-bucket local sort (auto: compact on strips of >= 4M "
@@ -89,6 +90,9 @@ def parse():
     ap.add_argument("--graphs", type=int, default=None, choices=[0, 1, 2],
                     help="GSR_OPT_FRAME_GRAPHS for every context slot (default: the library's): "
                          "0 direct, 1 recorded graphs, 2 the deferred-K chains launched directly")
+    ap.add_argument("--second-stream", type=int, default=None, choices=[0, 1],
+                    help="GSR_OPT_SECOND_STREAM of the in-flight frames (default: FramePipeline's "
+                         "choice -- off at depth >= 3 without frame graphs)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU-oracle time to sample for cpu_baseline (whole frames; at least one)")
     return ap.parse_args()
@@ -358,6 +362,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.inflight is None:
+        # full frames: four in flight, each on one stream (DESIGN.md decision 13); strip frames
+        # (a rank of an N-GPU frame): two, with second streams and frame graphs (decision 12)
+        args.inflight = 2 if (world > 1 or args.sim_strip) else 4
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         if world == 1:
             raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
@@ -390,7 +398,8 @@ def main():
     # strip frames (a rank of an N-GPU frame, or the simulated strip) replay frame graphs: with
     # two in flight a strip rank's rate is then steady instead of bimodal run to run (DESIGN.md
     # decision 12); full frames keep direct launches
-    pipe = FramePipeline(args.inflight, dev, graphs=args.inflight >= 2 and (world > 1 or bool(args.sim_strip)))
+    strip_graphs = args.inflight >= 2 and (world > 1 or bool(args.sim_strip))
+    pipe = None  # (created below: after the serial passes on one GPU)
 
     def step(i):
         with pipe.frame() as slot:
@@ -425,22 +434,61 @@ def main():
         opt(_lib.GSR_OPT_BLEND_FAST, {"exact": 0, "fast": 1}[args.blend])
         opt(_lib.GSR_OPT_DEPTH_SORT,
             {"auto": -1, "lsd": 0, "compact": 1, "msd": 2, "compact-msd": 3}[args.depth_sort])
-        if args.graphs is not None:
-            opt(_lib.GSR_OPT_FRAME_GRAPHS, args.graphs)
     # frame graphs: the pipeline's choice (strip frames in flight) unless --graphs; the serial
-    # pass below renders as a caller without the pipeline does (direct launches)
-    graphs_inflight = args.graphs if args.graphs is not None else int(pipe.graphs)
+    # passes render as a caller without the pipeline does (direct launches)
+    graphs_inflight = args.graphs if args.graphs is not None else int(strip_graphs)
     graphs_serial = args.graphs if args.graphs is not None else 0
+    names = _lib.stage_names()
+    buf = (ctypes.c_float * len(names))()
+
+    def serial_passes(rows):
+        """(2) Serial frame rate: one frame in flight (slot 0, the caller's stream, no gather,
+        the second stream on: a lone frame overlaps its own two halves) -- the frame time of a
+        viewer that renders each frame before starting the next; (3) the per-stage breakdown
+        (events at every stage boundary) of 30 more such forwards."""
+        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_FRAME_GRAPHS, graphs_serial),
+                   "gsr_set_option")
+        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_SECOND_STREAM, 1), "gsr_set_option")
+        torch.cuda.synchronize()
+        n_serial = 100
+        t1 = time.perf_counter()
+        for i in range(n_serial):
+            scene.render(i, rows, radii=rows is None)
+        torch.cuda.synchronize()
+        ms = 1e3 * (time.perf_counter() - t1) / n_serial
+        _lib.check(lib.gsr_set_timing(ctx, 1), "gsr_set_timing")
+        torch.cuda.synchronize()
+        for i in range(30):
+            scene.render(i, rows, radii=rows is None)
+        torch.cuda.synchronize()
+        _lib.check(lib.gsr_stage_times(ctx, buf, len(names)), "gsr_stage_times")
+        _lib.check(lib.gsr_set_timing(ctx, 0), "gsr_set_timing")
+        return ms, {n: float(buf[i]) for i, n in enumerate(names)}
 
     # The untimed diagnostic passes run first, so the device has been rendering for ~200 frames
     # when the timed region starts: a run of 20 timed frames after 5 warmup frames measured
     # 3,160-3,250 frames/s against 3,670-3,720 after 100+ frames of rendering (the same binary;
     # the GPU settles over the first ~30 ms of load), and the metric is the steady frame rate of
     # a viewer that keeps rendering.  Their sizes are fixed (not tied to --steps) for that reason.
+    # One GPU: the serial passes come first (after 64 untimed serial frames), before the
+    # pipeline's streams exist -- a stream's hardware queue is fixed when it is created, and a
+    # second stream created after four one-stream frame streams shared a queue with the caller's
+    # stream (serial 0.31 -> 0.6 ms, tools/lab/stream_probe.py).  Strip ranks (N > 1) time them
+    # after pass (1), on the split those frames ended with.
+    if world == 1:
+        for i in range(64):
+            scene.render(i, rows, radii=rows is None)
+        serial_ms, stage_ms = serial_passes(rows)
+    pipe = FramePipeline(args.inflight, dev, graphs=strip_graphs,
+                         second_stream=None if args.second_stream is None
+                         else bool(args.second_stream))
+    for c in ctxs:
+        if args.graphs is not None:
+            _lib.check(lib.gsr_set_option(c, _lib.GSR_OPT_FRAME_GRAPHS, args.graphs),
+                       "gsr_set_option")
+
     # (1) The blend's event time with frames in flight (events around the blend on every 8th
     # forward of slot 0; these frames run on the stream path).
-    names = _lib.stage_names()
-    buf = (ctypes.c_float * len(names))()
     n_pre = 0
     _lib.check(lib.gsr_set_timing(ctx, 2), "gsr_set_timing")
     for i in range(64):
@@ -451,33 +499,16 @@ def main():
     _lib.check(lib.gsr_stage_times(ctx, buf, len(names)), "gsr_stage_times")
     _lib.check(lib.gsr_set_timing(ctx, 0), "gsr_set_timing")
     blend_ms_timed = float(buf[names.index("blend")])
-    if balancer is not None:  # the split these frames ended with (for the serial passes)
-        rows = balancer.current[rank]
-        if rows[1] <= rows[0]:
-            rows = None
-
-    # (2) Serial frame rate: one frame in flight (slot 0, the caller's stream, no gather) -- the
-    # frame time of a viewer that renders each frame before starting the next.
-    _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_FRAME_GRAPHS, graphs_serial), "gsr_set_option")
-    torch.cuda.synchronize()
-    n_serial = 100
-    t1 = time.perf_counter()
-    for i in range(n_serial):
-        scene.render(i, rows, radii=rows is None)
-    torch.cuda.synchronize()
-    serial_ms = 1e3 * (time.perf_counter() - t1) / n_serial
-
-    # (3) Per-stage breakdown (events at every stage boundary): serial forwards on slot 0 (no
-    # frame overlap, no gather), so each stage's events bracket that stage alone.
-    _lib.check(lib.gsr_set_timing(ctx, 1), "gsr_set_timing")
-    torch.cuda.synchronize()
-    for i in range(30):
-        scene.render(i, rows, radii=rows is None)
-    torch.cuda.synchronize()
-    _lib.check(lib.gsr_stage_times(ctx, buf, len(names)), "gsr_stage_times")
-    _lib.check(lib.gsr_set_timing(ctx, 0), "gsr_set_timing")
-    stage_ms = {n: float(buf[i]) for i, n in enumerate(names)}
-    _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_FRAME_GRAPHS, graphs_inflight), "gsr_set_option")
+    if world > 1:
+        if balancer is not None:  # the split these frames ended with (for the serial passes)
+            rows = balancer.current[rank]
+            if rows[1] <= rows[0]:
+                rows = None
+        serial_ms, stage_ms = serial_passes(rows)
+        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_FRAME_GRAPHS, graphs_inflight),
+                   "gsr_set_option")
+        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_SECOND_STREAM, int(pipe.second_stream)),
+                   "gsr_set_option")
 
     # Warmup: W frames of the timed loop's own kind (in flight, gathered).
     for i in range(args.warmup):
@@ -588,8 +619,12 @@ def main():
         "stage_ms_note": "HIP events at every stage boundary, separate 30-frame serial pass "
                          "(each event adds a few us); the timed region records no events",
         "inflight": args.inflight,
-        "timed_after": "64 in-flight + 130 serial untimed diagnostic frames (blend events, serial "
-                       "rate, stage events), then the W warmup frames",
+        "second_stream": pipe.second_stream,
+        "timed_after": ("194 serial (64 untimed, 100 for the serial rate, 30 with stage events) "
+                        "then 64 in-flight (blend events) untimed diagnostic frames, then the W "
+                        "warmup frames" if world == 1 else
+                        "64 in-flight (blend events) + 130 serial (rate, stage events) untimed "
+                        "diagnostic frames, then the W warmup frames"),
         "strip_layout": (None if balancer is None else
                          {"tile_rows": [list(t) for t in balancer.current],
                           "rebalances": len(balancer.history),

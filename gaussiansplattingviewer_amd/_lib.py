@@ -21,6 +21,7 @@ GSR_OPT_BLEND_FAST = 2
 GSR_OPT_DEPTH_SORT = 11
 GSR_OPT_TIGHT_BINNING = 13
 GSR_OPT_FRAME_GRAPHS = 14
+GSR_OPT_SECOND_STREAM = 15
 
 # Symbols include/gsr.h declares (checked by the CPU test suite).
 EXPORTED_SYMBOLS = (

@@ -80,6 +80,10 @@ constexpr int64_t kCompactP = 4 << 20;
 #define GSR_MSD_MAX_D 25
 #endif
 constexpr uint32_t kMsdMaxD = GSR_MSD_MAX_D;
+// The MSD local sort keeps its wide form (8192 LDS slots) for this many frames after one whose
+// buckets crowded the narrow form's 4096 (C5: serial 0.342 -> 0.315 ms; the narrow form's
+// smaller LDS keeps C3 even, profiles/r05w_ab_local_slots.txt).
+constexpr uint32_t kCrowdFrames = 8;
 
 const char *kStageNames[kAllStages] = {"preprocess", "depth_sort", "scan",  "duplicate",
                                        "tile_sort",  "ranges",     "blend", "color"};
@@ -138,6 +142,7 @@ struct gsr_context {
     uint64_t *h_total = nullptr;
     unsigned long long *d_hostK = nullptr;  // device view of h_total + 2
     unsigned long long *d_hostD = nullptr;  // device view of h_total + 4
+    unsigned long long *d_hostCrowd = nullptr;  // device view of h_total + 1
     uint32_t sort_tag = 0;                  // frames rendered on this context (the pinned tags)
     // the bits of the last frame's kept depth keys' range and the bits in which they differ
     // (wait_K); the first frame, with no history, takes the LSD sort, which any spread of depths
@@ -163,9 +168,17 @@ struct gsr_context {
     int64_t timed_frames = 0;
     hipEvent_t ev[kTimingRing][kStages + 1] = {};
     hipEvent_t ev_color[kTimingRing][2] = {};
-    // second stream (lowest priority): pair count, tile ranges and colour, between a fork after
-    // the preprocess and a join before the blend
+    // second stream: pair count, tile ranges and colour, between a fork after the preprocess and
+    // a join before the blend.  Created on the first forward that uses it; GSR_OPT_SECOND_STREAM
+    // 0 runs that work on the frame's stream and destroys it, freeing its hardware queue for
+    // another frame in flight.  Normal priority, as the callers' streams: a stream's hardware
+    // queue is picked when it is created among the queues of its priority, and a low-priority
+    // second stream held one of the process's 4 queues apart from them, so four one-stream frame
+    // streams created after it shared three (C3 depth 4: ~3,300-3,550 against ~4,090 frames/s,
+    // profiles/r05y_stream_probe.txt, r05z2_ab_aux_priority.txt)
+    int second_stream = 1;
     hipStream_t aux = nullptr;
+    int aux_priority = 0;
     hipEvent_t fork = nullptr, join = nullptr;
     hipEvent_t compacted = nullptr;  // the compacted ids are written (main -> second stream)
     // frame graphs (GSR_OPT_FRAME_GRAPHS, DESIGN.md decision 12): the frame stream's chain after
@@ -287,6 +300,7 @@ struct Frame {
     bool graph = false;  // this forward replays recorded frame graphs (forward_graph)
     int col_shift;      // column pairs: packed word = strip row << col_shift | Gaussian id
     uint32_t tag;       // this frame's tag for the pinned words
+    bool wide_local;    // the MSD local sort's 8192-slot form (crowded buckets lately)
     GsrPreprocessArgs pa;
     bool tight;  // tight binning: pairs only over the span words (needs the column-first form)
     uint64_t K = 0;   // upstream's num_rendered
@@ -457,6 +471,13 @@ int setup_frame(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     f.tag = ++ctx->sort_tag;
     if (f.tag == 0) f.tag = ++ctx->sort_tag;  // 0 is the pinned words' initial value
     pa.k_tag = f.tag;
+    // the local sort's wide form while one of the last kCrowdFrames frames' sorts found buckets
+    // of 513-1024 keys crowding a group past 4096 LDS slots (the flag of the frame before this
+    // one may not have landed yet: the form is only a speed choice)
+    {
+        const uint32_t crowd = (uint32_t)__atomic_load_n(&ctx->h_total[1], __ATOMIC_ACQUIRE);
+        f.wide_local = crowd != 0u && f.tag - crowd <= kCrowdFrames;
+    }
     return GSR_OK;
 }
 
@@ -486,7 +507,8 @@ int launch_depth_sort(gsr_context *ctx, const Frame &f, int p0, int p1) {
         if (p0 != 0) return GSR_OK;  // (no later passes)
         e = gsr_depth_sort_msd(f.pa.sort_keys, f.P, f.main_publish ? nullptr : keybits, nb,
                                ds_a, ds_b, perm, hist, digit_total, ctl, f.s,
-                               f.graph ? nullptr : ctx->d_hostD, f.tag);
+                               f.graph ? nullptr : ctx->d_hostD, f.tag,
+                               f.graph ? nullptr : ctx->d_hostCrowd, f.graph ? 0 : f.wide_local);
     } else {  // (frame graphs queue every pass; the host reads no D)
         e = gsr_depth_sort(f.pa.sort_keys, f.P, 1, ds_a, ds_b, perm, hist, digit_total, ctl, p0,
                            p1, f.s, f.graph ? nullptr : ctx->d_hostD, f.tag);
@@ -540,6 +562,7 @@ int aux_chain(gsr_context *ctx, const Frame &f, hipStream_t as, const uint32_t *
 }
 
 int launch_second_stream(gsr_context *ctx, const Frame &f) {
+    if (!ctx->second_stream) return aux_chain(ctx, f, f.s, nullptr);  // in order, same stream
     hipStream_t as = ctx->aux;
     GSR_HIP(hipStreamWaitEvent(as, ctx->fork, 0), "hipStreamWaitEvent(fork)");
     GSR_TRY(aux_chain(ctx, f, as, nullptr));
@@ -588,7 +611,7 @@ int64_t list_capacity(int64_t n, int64_t cap) {
 int wait_K(gsr_context *ctx, Frame &f) {
     uint64_t tagv = 0;
     if (!spin_on(&ctx->h_total[7], [&](uint64_t v) { return v == f.tag; }, tagv))
-        GSR_HIP(hipStreamSynchronize(f.main_publish ? f.s : ctx->aux),
+        GSR_HIP(hipStreamSynchronize(f.main_publish || !ctx->second_stream ? f.s : ctx->aux),
                 "hipStreamSynchronize(pair count)");
     f.K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
     ctx->last_Dr = (uint32_t)__atomic_load_n(&ctx->h_total[6], __ATOMIC_ACQUIRE);
@@ -772,7 +795,7 @@ void finish_frame(gsr_context *ctx, const Frame &f, gsr_outputs *out) {
 // compaction (its colour pass waits on a mid-chain event of the frame stream), no rgb output
 // (the colour pass's).
 bool graph_eligible(const gsr_context *ctx, const Frame &f, const gsr_outputs *out) {
-    return ctx->graphs && ctx->list_cap > 0 && f.colpairs && !f.dbg && f.tmode != 1 &&
+    return ctx->graphs && ctx->second_stream && ctx->list_cap > 0 && f.colpairs && !f.dbg && f.tmode != 1 &&
            !f.compact_sort && !f.color_ids && !out->rgb && f.P > 0;
 }
 
@@ -831,7 +854,7 @@ int drain_retired(gsr_context *ctx, hipStream_t s, bool force) {
     if (ctx->graph_retired.empty() || (!force && ctx->graph_retired.size() < kGraphRetired))
         return GSR_OK;
     GSR_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(graphs)");
-    GSR_HIP(hipStreamSynchronize(ctx->aux), "hipStreamSynchronize(graphs)");
+    if (ctx->aux) GSR_HIP(hipStreamSynchronize(ctx->aux), "hipStreamSynchronize(graphs)");
     for (hipGraphExec_t ge : ctx->graph_retired) (void)hipGraphExecDestroy(ge);
     ctx->graph_retired.clear();
     return GSR_OK;
@@ -1012,6 +1035,9 @@ int forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings 
     Frame f;
     ctx->have_forward = false;
     GSR_TRY(setup_frame(ctx, g, st, out, s, f));
+    if (ctx->second_stream && !ctx->aux)
+        GSR_HIP(hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking, ctx->aux_priority),
+                "hipStreamCreateWithPriority(second stream)");
     f.graph = f.P > 0 && graph_eligible(ctx, f, out);
     if (f.graph) {
         GSR_TRY(drain_retired(ctx, s, false));
@@ -1060,7 +1086,7 @@ int forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings 
     GSR_TRY(launch_depth_sort(ctx, f, 0, 1));
     JoinGuard guard{s, ctx->join, false};
     GSR_TRY(launch_second_stream(ctx, f));
-    guard.armed = true;
+    guard.armed = ctx->second_stream != 0;
     // D (the bits in which the kept depth keys differ) arrives in pinned memory from pass 0's
     // scan, tagged with this frame, while pass 0's downsweep runs: the host then queues only the
     // passes D needs.  Without it every pass is queued and the unneeded ones exit at once.
@@ -1085,7 +1111,8 @@ int forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings 
 
     // ---- 6. join: the blend reads the colours and the second-stream ranges
     guard.armed = false;
-    GSR_HIP(hipStreamWaitEvent(s, ctx->join, 0), "hipStreamWaitEvent(join)");
+    if (ctx->second_stream)
+        GSR_HIP(hipStreamWaitEvent(s, ctx->join, 0), "hipStreamWaitEvent(join)");
     GSR_TRY(stage_end(ctx, f, 5));
 
     // ---- 7. blend
@@ -1120,20 +1147,23 @@ int gsr_create(gsr_context **out) {
         hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->d_hostK), ctx->h_total + 2, 0) !=
             hipSuccess ||
         hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->d_hostD), ctx->h_total + 4, 0) !=
-            hipSuccess) {
+            hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->d_hostCrowd), ctx->h_total + 1,
+                                0) != hipSuccess) {
         (void)hipGetLastError();
         delete ctx;
         return fail(GSR_E_HIP, "gsr_create: hipHostMalloc failed");
     }
     std::memset(ctx->h_total, 0, 8 * sizeof(uint64_t));  // tag 0 never matches a frame
+#ifdef GSR_AUX_LOW_PRIORITY  // lab: the second stream at the lowest priority (rounds 2-5)
     int prio_least = 0, prio_greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) {
         (void)hipGetLastError();
         prio_least = 0;
     }
-    bool ok = hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking, prio_least) ==
-                  hipSuccess &&
-              hipMalloc(&ctx->frame_words.p, 64) == hipSuccess &&
+    ctx->aux_priority = prio_least;
+#endif
+    bool ok = hipMalloc(&ctx->frame_words.p, 64) == hipSuccess &&
               hipMemset(ctx->frame_words.p, 0, 64) == hipSuccess &&
               // stream-to-stream hand-offs on one device: a device-scope release suffices
               hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming | hipEventReleaseToDevice) ==
@@ -1204,6 +1234,16 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
             ctx->fast = (int)value;
             return GSR_OK;
         case GSR_OPT_TIGHT_BINNING: ctx->tight = value ? 1 : 0; return GSR_OK;
+        case GSR_OPT_SECOND_STREAM:
+            if (value < 0 || value > 1)
+                return fail(GSR_E_INVALID, "gsr_set_option: second stream 0..1");
+            ctx->second_stream = (int)value;
+            if (!value && ctx->aux) {  // (drained first: its last frame's work may still run)
+                GSR_HIP(hipStreamSynchronize(ctx->aux), "hipStreamSynchronize(second stream)");
+                GSR_HIP(hipStreamDestroy(ctx->aux), "hipStreamDestroy(second stream)");
+                ctx->aux = nullptr;
+            }
+            return GSR_OK;
         case GSR_OPT_FRAME_GRAPHS:
             if (value < 0 || value > 2) return fail(GSR_E_INVALID, "gsr_set_option: graphs 0..2");
             ctx->graphs = (int)value;

@@ -554,23 +554,31 @@ __global__ __launch_bounds__(1024) void k_ds_bits(const uint2 *__restrict__ keyb
 }
 
 constexpr int kLGroup = kDW;                // buckets per k_ds_local block: one per wave
-constexpr int kLWave = 512;                 // keys a wave sorts alone (8 per lane)
+constexpr int kLWave = 1024;                // keys a wave sorts alone (16 per lane)
 constexpr int kLIt = 8;                     // elements per lane of an in-LDS bucket sort
 constexpr int kLCap = kDThreads * kLIt;     // 4096 elements sorted in LDS at once
 constexpr int kLSub = kDSub;                // 6-bit sub-passes
+// LDS keys (and ids) the waves' slices share: 4096 (45 KB a block), or 8192 (77 KB) on frames
+// whose buckets of 513-1024 keys crowd a group past 4096 (k_ds_local's wide form, chosen by the
+// host from the flag the previous frames raised)
+constexpr int kLSlotsNarrow = kLCap, kLSlotsWide = 2 * kLCap;
+static_assert(kLCap >= kDW * 512, "every bucket of <= 512 keys gets a wave slice");
 
+template <int kSlots>
 struct LocalSmem {
-    uint32_t keys[kLCap], vals[kLCap];
+    uint32_t keys[kSlots], vals[kSlots];
     RadixTileSmem<kDW, kLIt> rt;  // 8-bit sub-passes (radix_tile_scatter, in LDS only)
     uint32_t wcnt[kDSubBins * kDW];
     uint32_t tmp[kDW];
     uint32_t start[kLGroup + 1];  // the group's bucket starts (+ its end)
+    int32_t slice[kLGroup];       // each bucket's wave slice (wave_slices), -1: the block's
     uint32_t base[kDSubBins], cstart[kDSubBins], ccount[kDSubBins];  // the slow path
 };
 
 // One sub-pass of `bits` (1..6) of the slow path's chunk ranking (runtime width).
+template <typename Smem>
 __device__ __forceinline__ int local_rank(const uint32_t (&k)[kLIt], const uint32_t (&v)[kLIt],
-                                          uint32_t keep, int shift, int bits, LocalSmem &sm) {
+                                          uint32_t keep, int shift, int bits, Smem &sm) {
     return tile_rank_scatter<0, kLIt>(k, v, keep, shift, sm.keys, sm.vals, sm.wcnt, sm.tmp, bits);
 }
 
@@ -578,9 +586,10 @@ __device__ __forceinline__ int local_rank(const uint32_t (&k)[kLIt], const uint3
 // in bucket order -- by the local key ((bucket - d0) << low) | (key & low mask) of `bits` bits,
 // in 8-bit sub-passes (radix_tile_scatter: element order wave, item, lane; elements past n carry
 // the largest key and sort last); the sorted ids go to perm[b0 ...].
+template <typename Smem>
 __device__ void local_sort_lds(const uint2 *__restrict__ src, uint32_t *__restrict__ perm,
                                uint32_t b0, uint32_t n, uint32_t shift_hi, uint32_t d0, int low,
-                               int bits, LocalSmem &sm) {
+                               int bits, Smem &sm) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t lmask = (1u << low) - 1u;
     uint32_t k[kLIt], v[kLIt];
@@ -619,9 +628,10 @@ __device__ void local_sort_lds(const uint2 *__restrict__ src, uint32_t *__restri
 // chunks: count the digits, scan, then per chunk rank it in LDS and place every digit's run at
 // that digit's running offset.  Only a degenerate scene (more than 8192 kept Gaussians sharing
 // the top 12 of the varying depth bits) takes it.
+template <typename Smem>
 __device__ void local_sort_big(uint2 *__restrict__ src, uint2 *__restrict__ tmp,
                                uint32_t *__restrict__ perm, uint32_t b0, uint32_t n, int low,
-                               LocalSmem &sm) {
+                               Smem &sm) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     if (low == 0) {
         for (uint32_t e = tid; e < n; e += kDThreads) perm[b0 + e] = src[b0 + e].y;
@@ -694,23 +704,26 @@ __device__ void local_sort_big(uint2 *__restrict__ src, uint2 *__restrict__ tmp,
 // no block barrier: the wavefront fences only keep the compiler from moving LDS accesses across
 // the hand-offs), scattered into the wave's LDS slice; the ids go to perm[b0 ...].
 template <int kIt>
-__device__ void wave_sort_bucket(const uint2 *__restrict__ src, uint32_t *__restrict__ perm,
+__device__ __forceinline__ void wave_sort_bucket(const uint2 *__restrict__ src, uint32_t *__restrict__ perm,
                                  uint32_t b0, uint32_t n, int low, uint32_t *s_keys,
                                  uint32_t *s_vals, uint32_t *cnt) {
     const int lane = threadIdx.x & 63;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t lmask = (1u << low) - 1u;
     static_assert(kIt * 64 <= kLWave, "the wave's LDS slice");
+    // 16 keys per lane: each key's rank rides in its bits 16+ (low <= 16, rank < 1024), so the
+    // lane holds 32 words instead of 48
+    constexpr bool kPack = kIt > 8;
+    constexpr uint32_t kKeyMask = kPack ? 0xFFFFu : 0xFFFFFFFFu;
     uint32_t k[kIt], v[kIt];
+    // no branches around the loads (the slots past n are masked by `valid` below): branches
+    // here make the compiler copy the whole key and id arrays at every join
 #pragma unroll
     for (int j = 0; j < kIt; ++j) {
         const uint32_t e = (uint32_t)(j * 64 + lane);
-        k[j] = v[j] = 0u;
-        if (e < n) {
-            const uint2 q = src[b0 + e];
-            k[j] = q.x & lmask;
-            v[j] = q.y;
-        }
+        const uint2 q = src[b0 + min(e, n - 1u)];
+        k[j] = q.x & lmask;
+        v[j] = q.y;
     }
     for (int sh = 0; sh < low; sh += kDSub) {
         const int bits = min(kDSub, low - sh);
@@ -718,11 +731,11 @@ __device__ void wave_sort_bucket(const uint2 *__restrict__ src, uint32_t *__rest
         cnt[lane] = 0u;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        uint32_t rank[kIt];
+        uint32_t rank[kPack ? 1 : kIt];
 #pragma unroll
         for (int j = 0; j < kIt; ++j) {
             const bool valid = (uint32_t)(j * 64 + lane) < n;
-            const uint32_t d = (k[j] >> sh) & mask;
+            const uint32_t d = (k[j] >> sh) & mask;  // (kPack: the rank bits are still 0 here)
             const uint64_t m0 = __ballot(valid);
             uint32_t mlo = (uint32_t)m0, mhi = (uint32_t)(m0 >> 32);
 #pragma unroll
@@ -735,7 +748,10 @@ __device__ void wave_sort_bucket(const uint2 *__restrict__ src, uint32_t *__rest
             }
             const uint64_t m = ((uint64_t)mhi << 32) | mlo;
             const uint32_t prior = cnt[d];
-            rank[j] = prior + (uint32_t)__popcll(m & lt);
+            if constexpr (kPack)
+                k[j] |= (prior + (uint32_t)__popcll(m & lt)) << 16;
+            else
+                rank[j] = prior + (uint32_t)__popcll(m & lt);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             if (valid) cnt[d] = prior + (uint32_t)__popcll(m);  // same value from every match
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -749,19 +765,17 @@ __device__ void wave_sort_bucket(const uint2 *__restrict__ src, uint32_t *__rest
 #pragma unroll
         for (int j = 0; j < kIt; ++j) {
             if ((uint32_t)(j * 64 + lane) >= n) continue;
-            const uint32_t pos = cnt[(k[j] >> sh) & mask] + rank[j];
-            s_keys[pos] = k[j];
+            const uint32_t kj = k[j] & kKeyMask;
+            const uint32_t pos = cnt[(kj >> sh) & mask] + (kPack ? k[j] >> 16 : rank[kPack ? 0 : j]);
+            s_keys[pos] = kj;
             s_vals[pos] = v[j];
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-        for (int j = 0; j < kIt; ++j) {
-            const uint32_t e = (uint32_t)(j * 64 + lane);
-            if (e < n) {
-                k[j] = s_keys[e];
-                v[j] = s_vals[e];
-            }
+        for (int j = 0; j < kIt; ++j) {  // (the slice's slots past n: stale, never valid)
+            k[j] = s_keys[j * 64 + lane];
+            v[j] = s_vals[j * 64 + lane];
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -773,18 +787,65 @@ __device__ void wave_sort_bucket(const uint2 *__restrict__ src, uint32_t *__rest
     }
 }
 
+// LDS slots a wave needs to sort a bucket of n keys alone (2, 4, 8 or 16 keys per lane: the
+// ranking work is per item), 0 when the block sorts it (past 1024 keys, or key bits above the 16
+// the 16-key form packs its ranks over)
+__device__ __forceinline__ uint32_t wave_slots(uint32_t n, int low) {
+    return n == 0u     ? 0u
+           : n <= 128u ? 128u
+           : n <= 256u ? 256u
+           : n <= 512u ? 512u
+           : (n <= (uint32_t)kLWave && low <= 16) ? (uint32_t)kLWave
+                                                  : 0u;
+}
+
+// The LDS slice (first slot) where the wave of each bucket of the group sorts it, -1 when the
+// block sorts it (one thread plans, from the group's bucket sizes in registers): the buckets of
+// <= 512 keys get theirs first (at most 8 x 512 slots), then those of <= 1024 keys in bucket
+// order while the `slots` last.  Returns whether a bucket of <= 1024 keys was left to the block.
+__device__ __forceinline__ bool wave_slices(const uint32_t (&cnt)[kLGroup], int low,
+                                            uint32_t slots, int32_t *slice) {
+    uint32_t used = 0u;
+    bool left = false;
+#pragma unroll
+    for (int i = 0; i < kLGroup; ++i) {
+        const uint32_t need = wave_slots(cnt[i], low);
+        slice[i] = -1;
+        if (need && need <= 512u) {
+            slice[i] = (int32_t)used;
+            used += need;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kLGroup; ++i) {
+        const uint32_t need = wave_slots(cnt[i], low);
+        if (need != (uint32_t)kLWave) continue;
+        if (used + need > slots) {
+            left = true;
+            continue;
+        }
+        slice[i] = (int32_t)used;
+        used += need;
+    }
+    return left;
+}
+
 // Block g: buckets [8 g, 8 g + 8) of the MSD pass's output (pairs in bucket order; bucket d
-// starts at the exclusive sum of digit_total[0, d)), one per wave: a bucket of <= 512 keys (all
-// of them at C3, D = 24: at most ~500) is sorted by its wave alone; larger ones (4K frames: up
-// to ~2,800) by the whole block in LDS after the waves, in 8-bit sub-passes; past 4096 keys by
-// the slow path.  D <= 12: the MSD pass was the whole sort.
-__global__ __launch_bounds__(kDThreads) void k_ds_local(uint2 *__restrict__ pairs,
-                                                        uint2 *__restrict__ tmp,
-                                                        uint32_t *__restrict__ perm,
-                                                        const uint32_t *__restrict__ ctl,
-                                                        const uint32_t *__restrict__ digit_total) {
+// starts at the exclusive sum of digit_total[0, d)), one per wave: a bucket of <= 1024 keys (all
+// of them at C3, D = 24: at most ~500; C5's up to ~870) is sorted by its wave alone in its own
+// slice of the block's kSlots LDS slots (wave_slices); the rest (4K frames: up to ~2,800 keys)
+// by the whole block in LDS after the waves, in 8-bit sub-passes; past 4096 keys by the slow
+// path.  D <= 12: the MSD pass was the whole sort.  A group whose buckets of 513-1024 keys do
+// not all fit 4096 slots stores the frame's tag to host_crowd (pinned; NULL: none), from which
+// the host picks the wide form for the next frames.  (128 VGPRs: the 16-key form's arrays fit
+// without spills.)
+template <int kSlots>
+__global__ __launch_bounds__(kDThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_ds_local(
+    uint2 *__restrict__ pairs, uint2 *__restrict__ tmp, uint32_t *__restrict__ perm,
+    const uint32_t *__restrict__ ctl, const uint32_t *__restrict__ digit_total,
+    unsigned long long *__restrict__ host_crowd, uint32_t tag) {
     GSR_CHAIN_ENTRY();
-    __shared__ LocalSmem sm;
+    __shared__ LocalSmem<kSlots> sm;
     // the bits below the MSD digit: the MSD pass's own shift (ctl[2]); 0 when D <= 12
     const int low = (int)ctl[2];
     if (low == 0) return;
@@ -802,33 +863,42 @@ __global__ __launch_bounds__(kDThreads) void k_ds_local(uint2 *__restrict__ pair
         uint32_t total;
         blockw_exclusive_scan<kDW>(acc, sm.tmp, total);
         if (tid == 0) {
-            uint32_t run = total;
+            uint32_t run = total, cnt[kLGroup];
+#pragma unroll
             for (int i = 0; i < kLGroup; ++i) {
+                cnt[i] = digit_total[d0 + i];
                 sm.start[i] = run;
-                run += digit_total[d0 + i];
+                run += cnt[i];
             }
             sm.start[kLGroup] = run;
+            const bool crowded = wave_slices(cnt, low, (uint32_t)kLSlotsNarrow, sm.slice);
+            if (kSlots != kLSlotsNarrow) wave_slices(cnt, low, (uint32_t)kSlots, sm.slice);
+            if (crowded && host_crowd)
+                __hip_atomic_store(host_crowd, (unsigned long long)tag, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __syncthreads();
     }
     {
         const uint32_t b0 = sm.start[w], bn = sm.start[w + 1] - b0;
-        // keys per lane by the bucket's size (the ranking work is per item): 2, 4 or 8
-        uint32_t *sk = sm.keys + w * kLWave, *sv = sm.vals + w * kLWave;
+        const int slice = sm.slice[w];
+        uint32_t *sk = sm.keys + slice, *sv = sm.vals + slice;
         uint32_t *sc = sm.wcnt + w * kDSubBins;
-        if (bn == 0u) {
+        if (slice < 0) {
         } else if (bn <= 128u) {
             wave_sort_bucket<2>(pairs, perm, b0, bn, low, sk, sv, sc);
         } else if (bn <= 256u) {
             wave_sort_bucket<4>(pairs, perm, b0, bn, low, sk, sv, sc);
-        } else if (bn <= (uint32_t)kLWave) {
-            wave_sort_bucket<kLWave / 64>(pairs, perm, b0, bn, low, sk, sv, sc);
+        } else if (bn <= 512u) {
+            wave_sort_bucket<8>(pairs, perm, b0, bn, low, sk, sv, sc);
+        } else {
+            wave_sort_bucket<16>(pairs, perm, b0, bn, low, sk, sv, sc);
         }
     }
     __syncthreads();
-    for (int i = 0; i < kLGroup; ++i) {  // the larger buckets, one at a time by the block
+    for (int i = 0; i < kLGroup; ++i) {  // the rest, one at a time by the block
         const uint32_t b0 = sm.start[i], bn = sm.start[i + 1] - b0;
-        if (bn <= (uint32_t)kLWave) continue;
+        if (bn == 0u || sm.slice[i] >= 0) continue;  // (a wave sorted it)
         if (bn <= (uint32_t)kLCap)
             local_sort_lds(pairs, perm, b0, bn, shift_hi, d0 + (uint32_t)i, low, low, sm);
         else
@@ -896,7 +966,8 @@ hipError_t gsr_depth_sort(const uint32_t *keys, int64_t n, int drop, uint2 *pair
 static void msd_launch(const uint32_t *keys, const uint32_t *ids_in, const uint32_t *d_n, int drop,
                        int64_t n, const uint2 *keybits, int64_t n_keybits, uint2 *pairs_a,
                        uint2 *pairs_b, uint32_t *perm, uint32_t *hist, uint32_t *digit_total,
-                       uint32_t *ctl, hipStream_t s, unsigned long long *host_D, uint32_t tag) {
+                       uint32_t *ctl, hipStream_t s, unsigned long long *host_D, uint32_t tag,
+                       unsigned long long *host_crowd, int wide) {
     const unsigned nt = (unsigned)((n + kDT - 1) / kDT);
     if (keybits)  // (else ctl[1], ctl[2] are set: gsr_launch_count_pairs on this stream)
         hipLaunchKernelGGL(k_ds_bits, dim3(1), dim3(1024), 0, s, keybits, n_keybits, ctl);
@@ -906,18 +977,23 @@ static void msd_launch(const uint32_t *keys, const uint32_t *ids_in, const uint3
                        0, digit_total, d_n, host_D, tag, 1);
     hipLaunchKernelGGL(k_ds_downsweep<true>, dim3(nt), dim3(kDThreads), 0, s, keys, pairs_a, perm,
                        n, drop, ctl, 0, hist, digit_total, ids_in, d_n, 1);
-    hipLaunchKernelGGL(k_ds_local, dim3(kDBins / kLGroup), dim3(kDThreads), 0, s, pairs_a, pairs_b,
-                       perm, ctl, digit_total);
+    if (wide)
+        hipLaunchKernelGGL(k_ds_local<kLSlotsWide>, dim3(kDBins / kLGroup), dim3(kDThreads), 0, s,
+                           pairs_a, pairs_b, perm, ctl, digit_total, host_crowd, tag);
+    else
+        hipLaunchKernelGGL(k_ds_local<kLSlotsNarrow>, dim3(kDBins / kLGroup), dim3(kDThreads), 0,
+                           s, pairs_a, pairs_b, perm, ctl, digit_total, host_crowd, tag);
 }
 
 hipError_t gsr_depth_sort_msd(const uint32_t *keys, int64_t n, const uint2 *keybits,
                               int64_t n_keybits, uint2 *pairs_a, uint2 *pairs_b, uint32_t *perm,
                               uint32_t *hist, uint32_t *digit_total, uint32_t *ctl, hipStream_t s,
-                              unsigned long long *host_D, uint32_t tag) {
+                              unsigned long long *host_D, uint32_t tag,
+                              unsigned long long *host_crowd, int wide) {
     if (n <= 0) return hipSuccess;
     if (n > (int64_t)UINT32_MAX) return hipErrorInvalidValue;
     msd_launch(keys, nullptr, nullptr, 1, n, keybits, n_keybits, pairs_a, pairs_b, perm, hist,
-               digit_total, ctl, s, host_D, tag);
+               digit_total, ctl, s, host_D, tag, host_crowd, wide);
     return hipGetLastError();
 }
 
@@ -947,7 +1023,7 @@ hipError_t gsr_depth_sort_compacted(const uint32_t *keys, int64_t n, uint32_t *b
         // (pairs_b holds keys_c / ids_c: only the slow local sort of a degenerate bucket uses it,
         // after the MSD pass has read them)
         msd_launch(keys_c, ids_c, ctl, 0, n, keybits, n_keybits, pairs_a, pairs_b, perm, hist,
-                   digit_total, ctl, s, host_D, tag);
+                   digit_total, ctl, s, host_D, tag, nullptr, 0);
         return hipGetLastError();
     }
     return ds_passes(keys_c, ids_c, ctl, n, 0, pairs_a, pairs_b, perm, hist, digit_total, ctl,

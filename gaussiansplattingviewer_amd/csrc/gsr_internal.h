@@ -372,11 +372,14 @@ hipError_t gsr_depth_sort(const uint32_t *keys, int64_t n, int drop, uint2 *pair
 // over the top 12 of the D varying bits (dropping the 0xFFFFFFFF keys), then every bucket sorted
 // by the remaining bits in LDS.  Same result, ctl and perm contract as gsr_depth_sort with drop;
 // pairs_a holds the bucketed pairs, pairs_b is scratch.  host_D as in gsr_depth_sort.  keybits
-// NULL: ctl[1] and ctl[2] are already set (gsr_launch_count_pairs with ds_ctl).
+// NULL: ctl[1] and ctl[2] are already set (gsr_launch_count_pairs with ds_ctl).  host_crowd
+// (optional, device view of pinned host memory): the local sort stores the tag there when its
+// buckets of 513-1024 keys crowd the 4096 LDS slots of a group; wide: the 8192-slot local sort.
 hipError_t gsr_depth_sort_msd(const uint32_t *keys, int64_t n, const uint2 *keybits,
                               int64_t n_keybits, uint2 *pairs_a, uint2 *pairs_b, uint32_t *perm,
                               uint32_t *hist, uint32_t *digit_total, uint32_t *ctl, hipStream_t s,
-                              unsigned long long *host_D = nullptr, uint32_t tag = 0);
+                              unsigned long long *host_D = nullptr, uint32_t tag = 0,
+                              unsigned long long *host_crowd = nullptr, int wide = 0);
 // Compacting front end for sparse key sets (strips): the kept keys of each 256-key block
 // (block_kept[b] of them, from the preprocess) are written in order to keys_c, their indices
 // to ids_c, and their count to ctl[0]; then the sort runs on those (gsr_depth_sort_compacted,

@@ -734,6 +734,14 @@ hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int waves_per_simd, hipS
     // a 4-wave block puts one wave on each SIMD: w blocks per CU = w waves per SIMD, held by
     // reserving 1/w of the CU's 160 KiB of LDS per block (1 KiB granules)
     size_t lds = 0;
+#ifdef GSR_COLOR_BLOCKS_PER_CU
+    // lab: cap the grid instead of reserving LDS (blocks land wherever a CU has wave slots)
+    if (waves_per_simd >= 1 && waves_per_simd < 8) {
+        const unsigned cap = 256u * GSR_COLOR_BLOCKS_PER_CU;
+        hipLaunchKernelGGL(k_color, dim3(g0 < cap ? g0 : cap), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
+#endif
     if (waves_per_simd >= 1 && waves_per_simd < 8) {
         lds = (size_t)(160 * 1024 / waves_per_simd) & ~(size_t)1023;
         if (lds > 64 * 1024) {

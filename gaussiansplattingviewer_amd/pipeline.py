@@ -7,6 +7,8 @@ the depth sort are short dependent launches that leave most of the 256 CUs idle,
 blend saturates the VALUs of every CU.  `FramePipeline` gives each in-flight frame its own
 stream and its own `gsr_context` slot (workspace + second stream, `_lib.context(dev, slot)`),
 so the next frame's preprocess / sort / binning fill the CUs the current blend leaves free.
+At depth >= 3 each frame keeps all its work on its own stream (no second stream), so the frames
+in flight never share the process's four hardware queues.
 Every frame is still rendered completely and bit-identically to a serial forward (tested):
 only the order in which the GPU interleaves independent frames changes, as in a swap chain.
 """
@@ -32,15 +34,26 @@ class FramePipeline:
     (`wait(stream_of_frame)`); `torch.cuda.synchronize()` waits for all of them.
     """
 
-    def __init__(self, depth: int = 2, device=None, graphs: bool = False):
+    def __init__(self, depth: int = 2, device=None, graphs: bool = False,
+                 second_stream: bool | None = None):
         if depth < 1:
             raise ValueError("depth must be >= 1")
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.device = dev
         self.depth = depth
+        self.count = 0
+        self.graphs = bool(graphs)
+        # second_stream (gsr.h GSR_OPT_SECOND_STREAM; default: off at depth >= 3 without graphs):
+        # a frame's tile ranges, blend order and colour on its context's second stream, or in
+        # order on the frame's own stream.  The process has GPU_MAX_HW_QUEUES = 4 hardware
+        # queues: two frames of two streams each fill them, and so do four frames of one stream
+        # each -- which keeps more independent work beside every blend (C3 3,955-3,975 ->
+        # 4,100-4,130 frames/s; four two-stream frames 3,850-3,900, three 3,910, and more
+        # hardware queues do not help: profiles/r05z3_ab_hw_queues.txt, DESIGN.md decision 13).
+        self.second_stream = (not (depth >= 3 and not self.graphs) if second_stream is None
+                              else bool(second_stream))
         self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev)
                                                             for _ in range(depth - 1)]
-        self.count = 0
         # graphs=True: frame graphs (gsr.h GSR_OPT_FRAME_GRAPHS 1) on the slots' contexts; the
         # host queues a frame in a few graph launches and reads K after the whole frame is
         # queued.  With two frames in flight that pays on strip frames (a C3 3/8 strip 8.5-10.8k
@@ -49,13 +62,15 @@ class FramePipeline:
         # -2 %, C4 even; profiles/r05l_ab_frame_graphs.txt, r05o_ab_graphs_configs.txt), and a
         # serial frame pays ~15 us of GPU time for graph dispatch.  Images are bit-identical
         # either way (tests/test_gpu_frame_graphs.py).
-        self.graphs = bool(graphs)
         from . import _lib
         index = dev.index if dev.index is not None else torch.cuda.current_device()
+        lib = _lib.load_library()
         for slot in range(depth):
-            _lib.check(_lib.load_library().gsr_set_option(
-                _lib.context(index, slot), _lib.GSR_OPT_FRAME_GRAPHS, int(self.graphs)),
-                "gsr_set_option")
+            ctx = _lib.context(index, slot)
+            _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_FRAME_GRAPHS, int(self.graphs)),
+                       "gsr_set_option")
+            _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_SECOND_STREAM,
+                                          int(self.second_stream)), "gsr_set_option")
 
     def frame(self):
         """Context manager for the next frame: enters its stream, yields its context slot."""

@@ -241,12 +241,19 @@ const char *gsr_stage_name(int i);
  *     Full frames only (a strip's replicated preprocess would write a record per Gaussian for
  *     one strip's lists).  num_rendered stays upstream's count; gsr_get_binning exports the
  *     tight lists (0 binds upstream's lists).
+ *   GSR_OPT_SECOND_STREAM (default 1): the frame's tile ranges, blend order and colour run on
+ *     the context's second stream (created on first use), beside the same frame's depth sort and
+ *     binning.  0: they run in order on the frame's own stream and the second stream is
+ *     destroyed, so the context holds one hardware queue instead of two -- with the process's
+ *     GPU_MAX_HW_QUEUES = 4, four frames in flight on four contexts then each have a queue of
+ *     their own (FramePipeline with depth >= 3; DESIGN.md decision 13).  Frame graphs need the
+ *     second stream and are not used while it is 0.  The image is the same either way.
  * The binning form is chosen per frame: column-first (the first tile-sort pass on (Gaussian,
  * tile column) segments, the second on packed (tile row, Gaussian id) words) up to 256 tile
  * columns and strip rows, else the per-pair form; both produce the same lists.  Ids 10 and 12
  * are retired (ABI 1's column-pairs and tight-binning options) and rejected. */
 enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_DEPTH_SORT = 11,
-       GSR_OPT_TIGHT_BINNING = 13, GSR_OPT_FRAME_GRAPHS = 14 };
+       GSR_OPT_TIGHT_BINNING = 13, GSR_OPT_FRAME_GRAPHS = 14, GSR_OPT_SECOND_STREAM = 15 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
 
 /* Frame-graph counters of a context: stats[0] forwards rendered by replaying graphs,

@@ -36,13 +36,14 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_option_ids_match_header():
-    """The GSR_OPT_* ids of include/gsr.h are the ones _lib exposes (ABI 2: five options -- the
-    frame graphs' id 14 added in round 5 -- ids 10 and 12 of ABI 1 retired)."""
+    """The GSR_OPT_* ids of include/gsr.h are the ones _lib exposes (ABI 2: six options -- the
+    frame graphs' id 14 and the second stream's id 15 added in round 5 -- ids 10 and 12 of ABI 1
+    retired)."""
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     ids = {k: int(v) for k, v in re.findall(r"\b(GSR_OPT_[A-Z_]+)\s*=\s*(\d+)", src)}
     mine = {k: getattr(_lib, k) for k in dir(_lib) if k.startswith("GSR_OPT_")}
-    assert ids == mine and len(ids) <= 5
+    assert ids == mine and len(ids) <= 6
     assert 10 not in ids.values() and 12 not in ids.values()
 
 

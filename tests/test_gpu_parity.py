@@ -435,12 +435,13 @@ def test_compacted_strip_colour_path(gpu, form):
 
 
 def test_msd_local_sort_tier_boundaries(gpu, oracle_mod):
-    """k_ds_local sorts a bucket with 2, 4 or 8 keys per lane by its size (<= 128, <= 256,
-    <= 512 keys; larger ones by the whole block): buckets of the MSD pass's top 12 key bits are
+    """k_ds_local sorts a bucket with 2, 4, 8 or 16 keys per lane by its size (<= 128, <= 256,
+    <= 512, <= 1024 keys with GSR_LOCAL_WAVE_KEYS 1024; larger ones by the whole block): buckets of the MSD pass's top 12 key bits are
     built with sizes on both sides of every boundary (depths 2..8: D = 24, bucket = key bits
     12..23), then the frame must match the oracle."""
     rng = np.random.default_rng(41)
-    sizes = [1, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512, 513, 700, 2000]
+    sizes = [1, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512, 513, 700, 1023, 1024, 1025,
+             2000, 4000]
     keys = [np.uint32(0x40000000 | (4095 << 12) | 2048)]  # the deepest key: bit 23 set, D = 24
     for i, n in enumerate(sizes):
         b = 16 + 211 * i  # well-separated buckets below 4095
@@ -459,7 +460,7 @@ def test_msd_local_sort_tier_boundaries(gpu, oracle_mod):
     D = int(np.bitwise_or.reduce(d) ^ np.bitwise_and.reduce(d)).bit_length()
     counts = np.bincount((d >> np.uint32(D - 12)) & np.uint32(4095), minlength=4096)
     assert D == 24, D
-    for edge in (128, 256, 512):  # sizes on both sides of every tier boundary
+    for edge in (128, 256, 512, 1024):  # sizes on both sides of every tier boundary
         assert ((counts > 0) & (counts <= edge) & (counts > edge - 3)).any(), (edge, counts[counts > 0])
         assert ((counts > edge) & (counts < edge + 3)).any(), (edge, counts[counts > 0])
     _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, 2)
@@ -468,3 +469,43 @@ def test_msd_local_sort_tier_boundaries(gpu, oracle_mod):
     finally:
         _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, -1)
     assert_parity(hip, orc)
+
+
+def test_msd_local_sort_lds_slices(gpu, oracle_mod):
+    """k_ds_local's waves sort buckets of <= 1024 keys in slices of the block's 4096 LDS slots
+    (wave_slice): the buckets of <= 512 keys first, then the larger ones while slots remain, the
+    rest by the whole block.  Groups of 8 buckets with eight ~900-key buckets (four fit), three
+    ~1000-key and five ~300-key ones (one fits), and a mix across the 512 / 1024 edges.  The
+    first frame's crowded groups switch the context to the 8192-slot form (all fit) for the
+    next frames: both forms must match the oracle."""
+    rng = np.random.default_rng(43)
+    groups = {100: [900] * 8, 101: [1000, 1000, 1000, 300, 300, 300, 300, 300],
+              102: [1024, 1025, 513, 512, 1, 0, 1023, 129]}
+    keys = [np.uint32(0x40000000), np.uint32(0x40000000 | (4095 << 12) | 2048)]  # min, max: D = 24
+    for gi, sizes in groups.items():
+        for j, n in enumerate(sizes):
+            b = gi * 8 + j
+            low = rng.integers(1, 4096, n).astype(np.uint32)
+            low[1::3] = low[0::3][: len(low[1::3])]  # ties
+            keys.append(np.uint32(0x40000000) | np.uint32(b << 12) | low)
+    keys = np.concatenate([np.atleast_1d(k) for k in keys]).astype(np.uint32)
+    P = len(keys)
+    g = synthetic_gaussians(P, 3, 43)
+    g.xyz[:, :2] = rng.uniform(-0.15, 0.15, (P, 2)).astype(np.float32)
+    g.xyz[:, 2] = np.float32(3.0) - keys.view(np.float32)
+    g.scale[:] = np.float32(0.005)
+    g.opacity[:] = np.float32(3.0)
+    s = scene_inputs(g, static_camera(320, 240, (0, 0, 3.0)), 3)
+    orc = run_oracle(oracle_mod, s)
+    d = orc["depths"][orc["radii"] > 0].view(np.uint32)
+    kmin = d.min()
+    Dr = int(d.max() - kmin).bit_length()
+    counts = np.bincount((d - kmin) >> np.uint32(Dr - 12), minlength=4096)
+    assert Dr == 24, Dr
+    assert (counts[800:808] > 512).sum() >= 6 and (counts[816:824] > 1024).any(), counts[800:824]
+    _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, 2)
+    try:
+        for _ in range(3):
+            assert_parity(run_hip(s, gpu), orc)
+    finally:
+        _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, -1)

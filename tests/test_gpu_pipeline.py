@@ -1,6 +1,7 @@
-"""GPU: frames in flight (FramePipeline, two context slots on two streams) render every frame
-bit-identically to serial forwards, on a moving camera (per-frame re-sort), full frames and
-strips; and the oracle agrees with the pipelined frames."""
+"""GPU: frames in flight (FramePipeline: context slots on streams of their own, each frame on
+one stream or with its second stream) render every frame bit-identically to serial forwards,
+on a moving camera (per-frame re-sort), full frames and strips; and the oracle agrees with the
+pipelined frames."""
 import numpy as np
 import pytest
 import torch
@@ -35,10 +36,13 @@ def _render(dg, cam, W, H, dev, slot=0, tile_rows=None):
         False, False, slot=slot, tile_rows=tile_rows)
 
 
-@pytest.mark.parametrize("depth,tile_rows,graphs", [(2, None, False), (3, None, False),
-                                                    (2, (3, 9), False), (2, None, True),
-                                                    (2, (3, 9), True)])
-def test_pipelined_frames_equal_serial(gpu, depth, tile_rows, graphs):
+# (depth >= 3 runs each frame on one stream, GSR_OPT_SECOND_STREAM 0; second_stream forces it)
+@pytest.mark.parametrize("depth,tile_rows,graphs,second_stream",
+                         [(2, None, False, None), (3, None, False, None), (4, None, False, None),
+                          (4, (3, 9), False, None), (2, None, False, False),
+                          (4, None, False, True), (2, (3, 9), False, None),
+                          (2, None, True, None), (2, (3, 9), True, None)])
+def test_pipelined_frames_equal_serial(gpu, depth, tile_rows, graphs, second_stream):
     P, W, H, n = 60_000, 640, 480, 9
     _, dg, cams = _scene(gpu, P, W, H, n, seed=11)
     serial = []
@@ -47,14 +51,17 @@ def test_pipelined_frames_equal_serial(gpu, depth, tile_rows, graphs):
         serial.append((r.num_rendered, r.color.clone(), r.radii.clone()))
     torch.cuda.synchronize()
 
-    pipe = FramePipeline(depth, gpu, graphs=graphs)  # (frame graphs: GSR_OPT_FRAME_GRAPHS 1)
+    pipe = FramePipeline(depth, gpu, graphs=graphs, second_stream=second_stream)
+    assert pipe.second_stream == (second_stream if second_stream is not None
+                                  else depth < 3 or graphs)
     piped = []
     for cam in cams:
         with pipe.frame() as slot:
             r = _render(dg, cam, W, H, gpu, slot=slot, tile_rows=tile_rows)
             piped.append((r.num_rendered, r.color, r.radii))
     torch.cuda.synchronize()
-    FramePipeline(depth, gpu, graphs=False)  # (later tests see direct launches again)
+    # (later tests see direct launches on two streams again)
+    FramePipeline(depth, gpu, graphs=False, second_stream=True)
     for (k0, c0, r0), (k1, c1, r1) in zip(serial, piped):
         assert k0 == k1
         assert torch.equal(r0, r1)
