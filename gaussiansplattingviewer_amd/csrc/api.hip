@@ -80,6 +80,11 @@ constexpr int64_t kCompactP = 4 << 20;
 #define GSR_MSD_MAX_D 25
 #endif
 constexpr uint32_t kMsdMaxD = GSR_MSD_MAX_D;
+// ... and of <= this many on one-stream frames (GSR_OPT_SECOND_STREAM 0, frames in flight): there
+// the frame's total work counts more than its critical path, and the MSD form's single pass
+// outweighs the block sorts of crowded buckets (c3r, Dr = 26, four frames in flight: 4,200 ->
+// 4,420 frames/s, while a serial frame loses 0.315 -> 0.342 ms; profiles/r05z5_ab_msd26.txt)
+constexpr uint32_t kMsdMaxDOneStream = GSR_MSD_MAX_D + 1;
 // The MSD local sort keeps its wide form (8192 LDS slots) for this many frames after one whose
 // buckets crowded the narrow form's 4096 (C5: serial 0.342 -> 0.315 ms; the narrow form's
 // smaller LDS keeps C3 even, profiles/r05w_ab_local_slots.txt).
@@ -440,11 +445,13 @@ int setup_frame(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     // the kept keys' range (key - min), which balances them while the depths span a few float
     // exponents (Dr <= 25: C2, C3, C5 -- whose near Gaussians cross depth 2.0, D = 31 but Dr =
     // 24-25; C5 in flight +4 %, profiles/r05q_ab_range_msd.txt); wider ranges crowd some buckets
-    // past the LDS sort (c3r, Dr = 26: serial 0.313 -> 0.340 ms), so they keep the LSD passes.
+    // past the LDS sort (c3r, Dr = 26: serial 0.313 -> 0.340 ms), so they keep the LSD passes --
+    // except on one-stream frames in flight, where the single pass wins (kMsdMaxDOneStream).
     // The choice follows the previous frame's range (the result is the same either way, only the
     // time differs)
-    f.msd_sort = ctx->depth_sort < 0 ? ctx->last_Dr <= (uint32_t)kMsdMaxD
-                                     : ctx->depth_sort >= 2;
+    f.msd_sort = ctx->depth_sort < 0
+                     ? ctx->last_Dr <= (ctx->second_stream ? kMsdMaxD : kMsdMaxDOneStream)
+                     : ctx->depth_sort >= 2;
     // (compacted strips keep the second stream's publish: on the C4 1/8 strip the main-stream
     // publish let the tile counts and colour start earlier, beside the depth sort, 80 -> 134 us)
     f.main_publish = f.msd_sort && !f.compact_sort;
@@ -521,7 +528,10 @@ int launch_depth_sort(gsr_context *ctx, const Frame &f, int p0, int p1) {
 // to the binning chain it overlaps (C3 two frames in flight 3,890-3,918 -> 3,947-3,954
 // frames/s, serial 0.317 -> 0.308 ms; C4 serial 2.09 -> 2.06 ms); 3 on a compacted strip
 // (C4 1/8 strip 0.481 -> 0.468 ms).  profiles/r04n_ab_color_waves.txt, DESIGN.md decision 7
-int color_waves_of(const Frame &f) { return f.color_ids ? 3 : 2; }
+#ifndef GSR_COLOR_WAVES_FULL
+#define GSR_COLOR_WAVES_FULL 2
+#endif
+int color_waves_of(const Frame &f) { return f.color_ids ? 3 : GSR_COLOR_WAVES_FULL; }
 
 // ---- the second stream: K, the tile ranges (column pairs), the colour -----------------------
 // The second stream's kernels on stream `as` (a frame graph records them on its capture
