@@ -1,6 +1,7 @@
 """Lab probe: frame rates of one process as the second streams of its context slots are created
 and destroyed (GSR_OPT_SECOND_STREAM) around FramePipeline depths 2 and 4, at C3.
-argv: scenario -- 'prior' renders on slot 0 before the pipeline exists, 'fresh' does not,
+argv: scenario -- 'prior' renders on slot 0 before the pipeline exists, 'prior_destroy' also
+destroys that second stream before creating the pipeline, 'fresh' renders nothing before it,
 'timing' is 'fresh' with the in-flight blend events (gsr_set_timing 2) bench.py records."""
 import os
 import sys
@@ -42,8 +43,10 @@ def opt(slot, v):
     _lib.check(lib.gsr_set_option(_lib.context(0, slot), _lib.GSR_OPT_SECOND_STREAM, v), "opt")
 
 
-if mode == "prior":
+if mode in ("prior", "prior_destroy"):
     print(mode, "serial ms before the pipeline:", serial(), serial())
+if mode == "prior_destroy":  # slot 0's second stream destroyed before the pipeline's streams exist
+    opt(0, 0)
 p4 = FramePipeline(4, dev)
 ctx0 = _lib.context(0, 0)
 if mode == "timing":
