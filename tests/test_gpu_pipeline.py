@@ -105,3 +105,28 @@ def test_pipeline_out_color_buffer(gpu):
             torch.zeros(3, device=gpu), dg["xyz"], None, dg["opacity"], dg["scale"], dg["rot"],
             1.0, None, cams[0]["view"], cams[0]["proj"], cams[0]["tx"], cams[0]["ty"], H, W,
             dg["sh"], 3, cams[0]["campos"], False, False, out_color=buf[:3 * H * W].view(3, W, H))
+
+
+def test_second_stream_option(gpu):
+    """GSR_OPT_SECOND_STREAM: 0 / 1 toggle (the second stream destroyed and created again), other
+    values rejected; a forward in either mode gives the same bits."""
+    from gaussiansplattingviewer_amd import _lib
+    P, W, H = 30_000, 480, 320
+    _, dg, cams = _scene(gpu, P, W, H, 2, seed=17)
+    lib = _lib.load_library()
+    ctx = _lib.context(0, 0)
+    assert lib.gsr_set_option(ctx, _lib.GSR_OPT_SECOND_STREAM, 2) != 0
+    assert lib.gsr_set_option(ctx, _lib.GSR_OPT_SECOND_STREAM, -1) != 0
+    out = []
+    try:
+        for v in (0, 1, 0, 1):
+            _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_SECOND_STREAM, v), "gsr_set_option")
+            r = _render(dg, cams[1], W, H, gpu)
+            out.append((r.num_rendered, r.color.clone(), r.radii.clone()))
+            torch.cuda.synchronize()
+    finally:
+        _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_SECOND_STREAM, 1), "gsr_set_option")
+    for k, c, rad in out[1:]:
+        assert k == out[0][0]
+        assert torch.equal(rad, out[0][2])
+        assert torch.equal(c.view(torch.int32), out[0][1].view(torch.int32))
