@@ -790,6 +790,9 @@ hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int waves_per_simd, hipS
 #endif
     if (waves_per_simd >= 1 && waves_per_simd < 8) {
         lds = (size_t)(160 * 1024 / waves_per_simd) & ~(size_t)1023;
+#ifdef GSR_COLOR_LDS_MIN  // lab: the least LDS that still keeps a (w + 1)-th block out of the CU
+        lds = ((size_t)(160 * 1024 / (waves_per_simd + 1)) & ~(size_t)1023) + 1024;
+#endif
 #ifdef GSR_COLOR_SLAB
         if (lds < kSlabBytes) lds = kSlabBytes;
         const void *kern = reinterpret_cast<const void *>(&k_color_slab);
