@@ -801,12 +801,13 @@ void finish_frame(gsr_context *ctx, const Frame &f, gsr_outputs *out) {
 // num_rendered) and re-renders an overflowed frame the direct way with a larger capacity, so
 // every returned image is complete.
 
-// Eligible forwards: column-first binning, a known capacity, no debug, no per-stage timing, no
+// Eligible forwards: the second stream on (the second chain is recorded and replayed there),
+// column-first binning, a known capacity, no debug, no per-stage timing, no
 // compaction (its colour pass waits on a mid-chain event of the frame stream), no rgb output
 // (the colour pass's).
 bool graph_eligible(const gsr_context *ctx, const Frame &f, const gsr_outputs *out) {
-    return ctx->graphs && ctx->second_stream && ctx->list_cap > 0 && f.colpairs && !f.dbg && f.tmode != 1 &&
-           !f.compact_sort && !f.color_ids && !out->rgb && f.P > 0;
+    return ctx->graphs && ctx->second_stream && ctx->list_cap > 0 && f.colpairs && !f.dbg &&
+           f.tmode != 1 && !f.compact_sort && !f.color_ids && !out->rgb && f.P > 0;
 }
 
 GraphKey graph_key(const gsr_context *ctx, const Frame &f) {
