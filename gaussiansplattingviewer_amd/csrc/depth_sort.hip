@@ -704,9 +704,10 @@ __device__ void local_sort_big(uint2 *__restrict__ src, uint2 *__restrict__ tmp,
 // no block barrier: the wavefront fences only keep the compiler from moving LDS accesses across
 // the hand-offs), scattered into the wave's LDS slice; the ids go to perm[b0 ...].
 template <int kIt>
-__device__ __forceinline__ void wave_sort_bucket(const uint2 *__restrict__ src, uint32_t *__restrict__ perm,
-                                 uint32_t b0, uint32_t n, int low, uint32_t *s_keys,
-                                 uint32_t *s_vals, uint32_t *cnt) {
+__device__ __forceinline__ void wave_sort_bucket(const uint2 *__restrict__ src,
+                                                 uint32_t *__restrict__ perm, uint32_t b0,
+                                                 uint32_t n, int low, uint32_t *s_keys,
+                                                 uint32_t *s_vals, uint32_t *cnt) {
     const int lane = threadIdx.x & 63;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t lmask = (1u << low) - 1u;
