@@ -130,3 +130,37 @@ def test_second_stream_option(gpu):
         assert k == out[0][0]
         assert torch.equal(rad, out[0][2])
         assert torch.equal(c.view(torch.int32), out[0][1].view(torch.int32))
+
+
+def test_one_stream_frames_clustered_scene(gpu):
+    """Four one-stream frames in flight on the clustered (c3r-like) scene, whose kept depth keys
+    span ~26 bits: those frames take the MSD depth sort (kMsdMaxDOneStream) where a serial
+    two-stream forward takes the LSD passes -- every frame must still be bit-identical."""
+    from gaussiansplattingviewer_amd.gaussian_data import clustered_scene
+    P, W, H, n = 120_000, 640, 480, 9
+    g = clustered_scene(P, 5)
+    up = lambda a: torch.as_tensor(np.ascontiguousarray(a)).to(gpu)  # noqa: E731
+    dg = dict(xyz=up(g.xyz), rot=up(g.rot), scale=up(g.scale), opacity=up(g.opacity),
+              sh=up(g.sh).reshape(P, -1, 3).contiguous())
+    cams = []
+    for i in range(n):
+        view, proj, campos, tx, ty = cuda_camera_inputs(static_camera(W, H, orbit_eye(i * 11, 1000)))
+        cams.append(dict(view=up(view), proj=up(proj), campos=up(campos), tx=tx, ty=ty))
+    serial = []
+    for cam in cams:
+        r = _render(dg, cam, W, H, gpu)
+        serial.append((r.num_rendered, r.color.clone(), r.radii.clone()))
+    torch.cuda.synchronize()
+    pipe = FramePipeline(4, gpu)
+    assert not pipe.second_stream
+    piped = []
+    for cam in cams:
+        with pipe.frame() as slot:
+            r = _render(dg, cam, W, H, gpu, slot=slot)
+            piped.append((r.num_rendered, r.color, r.radii))
+    torch.cuda.synchronize()
+    FramePipeline(4, gpu, graphs=False, second_stream=True)
+    for (k0, c0, r0), (k1, c1, r1) in zip(serial, piped):
+        assert k0 == k1
+        assert torch.equal(r0, r1)
+        assert torch.equal(c0.view(torch.int32), c1.view(torch.int32))
