@@ -509,3 +509,23 @@ def test_msd_local_sort_lds_slices(gpu, oracle_mod):
             assert_parity(run_hip(s, gpu), orc)
     finally:
         _set_option(gpu, _lib.GSR_OPT_DEPTH_SORT, -1)
+
+
+def test_one_stream_forward_outputs(gpu, oracle_mod):
+    """GSR_OPT_SECOND_STREAM 0: the second stream's kernels run in order on the frame's stream.
+    Every output -- image, radii, the rgb extra, the lists -- equals the two-stream forward's, and
+    matches the oracle."""
+    s = scene_inputs(synthetic_gaussians(20_000, 3, 51), static_camera(320, 240, (0.2, 0.1, 3.5)), 3)
+    two = run_hip(s, gpu)
+    _set_option(gpu, _lib.GSR_OPT_SECOND_STREAM, 0)
+    try:
+        one = run_hip(s, gpu)
+    finally:
+        _set_option(gpu, _lib.GSR_OPT_SECOND_STREAM, 1)
+    assert one.keys() == two.keys()
+    for k in two:
+        if isinstance(two[k], np.ndarray):
+            np.testing.assert_array_equal(one[k], two[k], err_msg=k)
+        else:
+            assert one[k] == two[k], k
+    assert_parity(one, run_oracle(oracle_mod, s))
