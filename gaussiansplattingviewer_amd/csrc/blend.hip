@@ -388,7 +388,13 @@ hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s) {
     const uint32_t n_work = 4u * a.grid_x * a.rows_tiles;
     const dim3 grid(xcd_grid(n_work));
     if (a.fast && !a.n_contrib)
+#ifdef GSR_BLEND_WAVES  // lab: cap the blend's waves per SIMD through dynamic LDS per block
+        hipLaunchKernelGGL((k_blend_q<true, false>), grid, dim3(64),
+                           ((160 * 1024 / (4 * GSR_BLEND_WAVES) + 1023) & ~1023) - 3072, s, a,
+                           n_work);
+#else
         hipLaunchKernelGGL((k_blend_q<true, false>), grid, dim3(64), 0, s, a, n_work);
+#endif
     else if (a.fast)
         hipLaunchKernelGGL((k_blend_q<true, true>), grid, dim3(64), 0, s, a, n_work);
     else
