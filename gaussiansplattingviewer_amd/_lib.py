@@ -14,7 +14,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # GSR_LIB: another build of the library (A/B builds in tools/ab.sh); default the in-tree libgsr.so
 LIB_PATH = os.environ.get("GSR_LIB") or os.path.join(_HERE, "libgsr.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 GSR_OPT_BLEND_CULL = 1
 GSR_OPT_BLEND_FAST = 2
@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_get_binning", "gsr_mark_visible", "gsr_depth_argsort",
     "gsr_set_timing", "gsr_stage_times", "gsr_stage_name", "gsr_set_option",
     "gsr_ply_probe", "gsr_ply_load", "gsr_disparity_colors", "gsr_pack_image",
-    "gsr_tile_row_pairs", "gsr_frame_graph_stats",
+    "gsr_tile_row_pairs", "gsr_frame_graph_stats", "gsr_get_option",
 )
 
 GSR_PACK_RGBA_F32 = 0
@@ -102,6 +102,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.gsr_stage_name.argtypes = [i32]
     lib.gsr_stage_name.restype = ctypes.c_char_p
     lib.gsr_set_option.argtypes = [vp, i32, i64]
+    lib.gsr_get_option.argtypes = [vp, i32, ctypes.POINTER(i64)]
     lib.gsr_frame_graph_stats.argtypes = [vp, ctypes.POINTER(i64), i32]
     lib.gsr_ply_probe.argtypes = [ctypes.c_char_p, ctypes.POINTER(GsrPlyInfo)]
     lib.gsr_ply_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(GsrPlyInfo), vp, vp, vp, vp, vp,
@@ -112,7 +113,7 @@ def _declare(lib: ctypes.CDLL) -> None:
                                    ctypes.c_int32, vp, vp]
     for name in ("gsr_disparity_colors", "gsr_pack_image", "gsr_create", "gsr_reserve", "gsr_forward", "gsr_get_binning",
                  "gsr_mark_visible", "gsr_depth_argsort", "gsr_set_timing", "gsr_tile_row_pairs",
-                 "gsr_stage_times", "gsr_set_option", "gsr_ply_probe", "gsr_ply_load",
+                 "gsr_stage_times", "gsr_set_option", "gsr_get_option", "gsr_ply_probe", "gsr_ply_load",
                  "gsr_frame_graph_stats"):
         getattr(lib, name).restype = i32
 
@@ -212,6 +213,17 @@ def frame_graph_stats(device_index: int = 0, slot: int = 0) -> dict:
     v = (ctypes.c_int64 * 4)()
     check(lib.gsr_frame_graph_stats(context(device_index, slot), v, 4), "gsr_frame_graph_stats")
     return {"graph_frames": v[0], "graphs_recorded": v[1], "overflows": v[2], "list_cap": v[3]}
+
+
+def get_option(ctx, option: int) -> int:
+    """The current value of a context option (gsr_get_option)."""
+    v = ctypes.c_int64()
+    check(load_library().gsr_get_option(ctx, option, ctypes.byref(v)), "gsr_get_option")
+    return int(v.value)
+
+
+def set_option(ctx, option: int, value: int) -> None:
+    check(load_library().gsr_set_option(ctx, option, int(value)), "gsr_set_option")
 
 
 def stage_names() -> list[str]:

@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -75,16 +76,13 @@ constexpr int64_t kWaitDPairs = 4 << 20;
 // (GSR_OPT_DEPTH_SORT auto): a 1/8 strip of C4 keeps ~1/8 of them (DESIGN.md decision 2).
 constexpr int64_t kCompactP = 4 << 20;
 // The MSD depth sort for frames whose previous frame's kept depth keys spanned a range of <= this
-// many bits (setup_frame; lab builds override it with -DGSR_MSD_MAX_D).
-#ifndef GSR_MSD_MAX_D
-#define GSR_MSD_MAX_D 25
-#endif
-constexpr uint32_t kMsdMaxD = GSR_MSD_MAX_D;
+// many bits (setup_frame).
+constexpr uint32_t kMsdMaxD = 25;
 // ... and of <= this many on one-stream frames (GSR_OPT_SECOND_STREAM 0, frames in flight): there
 // the frame's total work counts more than its critical path, and the MSD form's single pass
 // outweighs the block sorts of crowded buckets (c3r, Dr = 26, four frames in flight: 4,200 ->
 // 4,420 frames/s, while a serial frame loses 0.315 -> 0.342 ms; profiles/r05z5_ab_msd26.txt)
-constexpr uint32_t kMsdMaxDOneStream = GSR_MSD_MAX_D + 1;
+constexpr uint32_t kMsdMaxDOneStream = kMsdMaxD + 1;
 // The MSD local sort keeps its wide form (8192 LDS slots) for this many frames after one whose
 // buckets crowded the narrow form's 4096 (C5: serial 0.342 -> 0.315 ms; the narrow form's
 // smaller LDS keeps C3 even, profiles/r05w_ab_local_slots.txt).
@@ -126,6 +124,14 @@ struct GraphEntry {
 
 struct gsr_context {
     int device = 0;
+    // One caller at a time: every entry point that reads or changes the context's workspace,
+    // options, pinned words or recorded graphs holds this (the `_C` extension renders with the
+    // GIL released, so two host threads may reach one device's context together).
+    std::mutex mu;
+    // The stream the last call that used the workspace ran on: a call on another stream first
+    // waits for the device (the workspace is stream-ordered on one stream at a time).
+    hipStream_t ws_stream = nullptr;
+    bool ws_stream_set = false;
     // per-Gaussian workspace
     DevBuf records, strip_rect, sort_keys, partials, total, hist, digit_total, bin, chunk_first,
         rect_sorted, pair_count;
@@ -183,7 +189,6 @@ struct gsr_context {
     // profiles/r05y_stream_probe.txt, r05z2_ab_aux_priority.txt)
     int second_stream = 1;
     hipStream_t aux = nullptr;
-    int aux_priority = 0;
     hipEvent_t fork = nullptr, join = nullptr;
     hipEvent_t compacted = nullptr;  // the compacted ids are written (main -> second stream)
     // frame graphs (GSR_OPT_FRAME_GRAPHS, DESIGN.md decision 12): the frame stream's chain after
@@ -201,6 +206,16 @@ struct gsr_context {
 };
 
 namespace {
+
+// Orders this call after the context's previous workspace user when the caller switched streams
+// (rare: a pipeline gives every stream its own context; a synchronisation only then).
+int order_stream(gsr_context *ctx, hipStream_t s) {
+    if (ctx->ws_stream_set && s != ctx->ws_stream)
+        GSR_HIP(hipDeviceSynchronize(), "hipDeviceSynchronize(stream switch)");
+    ctx->ws_stream = s;
+    ctx->ws_stream_set = true;
+    return GSR_OK;
+}
 
 // Grow-only device buffer.  Both streams are drained first so no in-flight kernel still reads
 // the old allocation.
@@ -528,10 +543,8 @@ int launch_depth_sort(gsr_context *ctx, const Frame &f, int p0, int p1) {
 // to the binning chain it overlaps (C3 two frames in flight 3,890-3,918 -> 3,947-3,954
 // frames/s, serial 0.317 -> 0.308 ms; C4 serial 2.09 -> 2.06 ms); 3 on a compacted strip
 // (C4 1/8 strip 0.481 -> 0.468 ms).  profiles/r04n_ab_color_waves.txt, DESIGN.md decision 7
-#ifndef GSR_COLOR_WAVES_FULL
-#define GSR_COLOR_WAVES_FULL 2
-#endif
-int color_waves_of(const Frame &f) { return f.color_ids ? 3 : GSR_COLOR_WAVES_FULL; }
+constexpr int kColorWavesFull = 2;
+int color_waves_of(const Frame &f) { return f.color_ids ? 3 : kColorWavesFull; }
 
 // ---- the second stream: K, the tile ranges (column pairs), the colour -----------------------
 // The second stream's kernels on stream `as` (a frame graph records them on its capture
@@ -991,11 +1004,13 @@ int find_graphs(gsr_context *ctx, const Frame &f, GraphEntry **out) {
 }
 
 constexpr int kOverflow = 1;  // forward_graph: the list outgrew the capacity (not rendered)
+constexpr int kNoGraphs = 2;  // forward_graph: recording failed before anything was queued
 
 int forward_graph(gsr_context *ctx, Frame &f, const gsr_raster_settings *st, gsr_outputs *out) {
     GraphEntry *e = nullptr;
     const bool replay = ctx->graphs == 1;  // 2: the same chains launched directly
-    if (replay) GSR_TRY(find_graphs(ctx, f, &e));
+    // a chain that cannot be recorded or instantiated leaves the frame to the direct path
+    if (replay && find_graphs(ctx, f, &e) != GSR_OK) return kNoGraphs;
     Frame g = graph_frame(ctx, f);
     const uint32_t *fw = static_cast<const uint32_t *>(ctx->frame_words.p);
     hipStream_t s = f.s;
@@ -1047,12 +1062,18 @@ int forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings 
     ctx->have_forward = false;
     GSR_TRY(setup_frame(ctx, g, st, out, s, f));
     if (ctx->second_stream && !ctx->aux)
-        GSR_HIP(hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking, ctx->aux_priority),
+        GSR_HIP(hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking, 0),
                 "hipStreamCreateWithPriority(second stream)");
     f.graph = f.P > 0 && graph_eligible(ctx, f, out);
     if (f.graph) {
         GSR_TRY(drain_retired(ctx, s, false));
-        const int rc = forward_graph(ctx, f, st, out);
+        int rc = forward_graph(ctx, f, st, out);
+        if (rc == kNoGraphs) {
+            // recording failed before anything of the frame was queued: this context launches
+            // the same deferred-K chains directly from now on (GSR_OPT_FRAME_GRAPHS 2)
+            ctx->graphs = 2;
+            rc = forward_graph(ctx, f, st, out);
+        }
         if (rc != kOverflow) return rc;
         // the list outgrew the capacity: nothing was binned or blended.  Grow the capacity and
         // render the frame again the direct way (the stream orders it after the skipped one)
@@ -1166,14 +1187,6 @@ int gsr_create(gsr_context **out) {
         return fail(GSR_E_HIP, "gsr_create: hipHostMalloc failed");
     }
     std::memset(ctx->h_total, 0, 8 * sizeof(uint64_t));  // tag 0 never matches a frame
-#ifdef GSR_AUX_LOW_PRIORITY  // lab: the second stream at the lowest priority (rounds 2-5)
-    int prio_least = 0, prio_greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) {
-        (void)hipGetLastError();
-        prio_least = 0;
-    }
-    ctx->aux_priority = prio_least;
-#endif
     bool ok = hipMalloc(&ctx->frame_words.p, 64) == hipSuccess &&
               hipMemset(ctx->frame_words.p, 0, 64) == hipSuccess &&
               // stream-to-stream hand-offs on one device: a device-scope release suffices
@@ -1182,7 +1195,8 @@ int gsr_create(gsr_context **out) {
               hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming | hipEventReleaseToDevice) ==
                   hipSuccess &&
               hipEventCreateWithFlags(&ctx->compacted,
-                                      hipEventDisableTiming | hipEventReleaseToDevice) == hipSuccess;
+                                      hipEventDisableTiming | hipEventReleaseToDevice) == hipSuccess &&
+              gsr_color_setup() == hipSuccess;
     // timing events only time: no system-scope fence (cache writeback) when they complete
     for (auto &set : ctx->ev)
         for (auto &e : set) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableSystemFence) == hipSuccess;
@@ -1228,6 +1242,7 @@ void gsr_destroy(gsr_context *ctx) {
 
 int gsr_reserve(gsr_context *ctx, int64_t P, int64_t K) {
     if (!ctx || P < 0 || K < 0) return fail(GSR_E_INVALID, "gsr_reserve: bad arguments");
+    std::lock_guard<std::mutex> lock(ctx->mu);
     GSR_TRY(reserve_P(ctx, P, nullptr));
     if (K > ctx->list_cap) ctx->list_cap = std::min<int64_t>((K + 4095) & ~(int64_t)4095,
                                                              (int64_t)UINT32_MAX - 4096);
@@ -1238,6 +1253,7 @@ int gsr_reserve(gsr_context *ctx, int64_t P, int64_t K) {
 
 int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
     if (!ctx) return fail(GSR_E_INVALID, "gsr_set_option: NULL context");
+    std::lock_guard<std::mutex> lock(ctx->mu);
     switch (option) {
         case GSR_OPT_BLEND_CULL: ctx->cull = value ? 1 : 0; return GSR_OK;
         case GSR_OPT_BLEND_FAST:
@@ -1269,8 +1285,24 @@ int gsr_set_option(gsr_context *ctx, int option, int64_t value) {
     }
 }
 
+int gsr_get_option(gsr_context *ctx, int option, int64_t *value) {
+    if (!ctx || !value) return fail(GSR_E_INVALID, "gsr_get_option: NULL argument");
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    switch (option) {
+        case GSR_OPT_BLEND_CULL: *value = ctx->cull; return GSR_OK;
+        case GSR_OPT_BLEND_FAST: *value = ctx->fast; return GSR_OK;
+        case GSR_OPT_TIGHT_BINNING: *value = ctx->tight; return GSR_OK;
+        case GSR_OPT_SECOND_STREAM: *value = ctx->second_stream; return GSR_OK;
+        case GSR_OPT_FRAME_GRAPHS: *value = ctx->graphs; return GSR_OK;
+        case GSR_OPT_DEPTH_SORT: *value = ctx->depth_sort; return GSR_OK;
+        default:
+            return fail(GSR_E_INVALID, "gsr_get_option: unknown option " + std::to_string(option));
+    }
+}
+
 int gsr_frame_graph_stats(gsr_context *ctx, int64_t *stats, int n) {
     if (!ctx || (!stats && n > 0)) return fail(GSR_E_INVALID, "gsr_frame_graph_stats: bad arguments");
+    std::lock_guard<std::mutex> lock(ctx->mu);
     const int64_t v[4] = {ctx->graph_frames, ctx->graph_records, ctx->graph_overflows,
                           ctx->list_cap};
     for (int i = 0; i < n && i < 4; ++i) stats[i] = v[i];
@@ -1279,6 +1311,7 @@ int gsr_frame_graph_stats(gsr_context *ctx, int64_t *stats, int n) {
 
 int gsr_set_timing(gsr_context *ctx, int enable) {
     if (!ctx) return fail(GSR_E_INVALID, "gsr_set_timing: NULL context");
+    std::lock_guard<std::mutex> lock(ctx->mu);
     if (enable < 0 || enable > 2) return fail(GSR_E_INVALID, "gsr_set_timing: mode 0..2");
     ctx->timing = enable;
     ctx->forwards = 0;
@@ -1290,6 +1323,7 @@ int gsr_set_timing(gsr_context *ctx, int enable) {
 // kTimingRing of them).  Waits for the last one.  Return value: number of stages.
 int gsr_stage_times(gsr_context *ctx, float *ms, int n) {
     if (!ctx || (!ms && n > 0)) return fail(GSR_E_INVALID, "gsr_stage_times: bad arguments");
+    std::lock_guard<std::mutex> lock(ctx->mu);
     if (ctx->timed_frames == 0) return fail(GSR_E_STATE, "gsr_stage_times: no timed forward yet");
     const int64_t frames = std::min<int64_t>(ctx->timed_frames, kTimingRing);
     const int64_t last = (ctx->timed_frames - 1) % kTimingRing;
@@ -1318,14 +1352,18 @@ int gsr_stage_times(gsr_context *ctx, float *ms, int n) {
 int gsr_forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings *st,
                 gsr_outputs *out, void *stream) {
     if (!ctx || !g || !st || !out) return fail(GSR_E_INVALID, "gsr_forward: NULL argument");
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    GSR_TRY(order_stream(ctx, static_cast<hipStream_t>(stream)));
     return forward(ctx, g, st, out, static_cast<hipStream_t>(stream));
 }
 
 int gsr_get_binning(gsr_context *ctx, uint32_t *point_list, uint32_t *point_tiles,
                     uint32_t *ranges, int64_t *list_entries, int32_t *num_tiles, void *stream) {
     if (!ctx) return fail(GSR_E_INVALID, "gsr_get_binning: NULL context");
+    std::lock_guard<std::mutex> lock(ctx->mu);
     if (!ctx->have_forward) return fail(GSR_E_STATE, "gsr_get_binning: no forward yet");
     hipStream_t s = static_cast<hipStream_t>(stream);
+    GSR_TRY(order_stream(ctx, s));
     const int64_t K = ctx->last_list;
     const uint64_t T = (uint64_t)ctx->last_gx * ctx->last_gy;
     const uint64_t off = (uint64_t)ctx->last_rb * ctx->last_gx;
@@ -1364,11 +1402,13 @@ int gsr_get_binning(gsr_context *ctx, uint32_t *point_list, uint32_t *point_tile
 
 int gsr_tile_row_pairs(gsr_context *ctx, uint32_t *row_pairs, int32_t n_rows, void *stream) {
     if (!ctx) return fail(GSR_E_INVALID, "gsr_tile_row_pairs: NULL context");
+    std::lock_guard<std::mutex> lock(ctx->mu);
     if (!ctx->have_forward) return fail(GSR_E_STATE, "gsr_tile_row_pairs: no forward yet");
     const uint32_t rows = ctx->last_re - ctx->last_rb;
     if (n_rows != (int32_t)rows || (rows > 0 && !row_pairs))
         return fail(GSR_E_INVALID, "gsr_tile_row_pairs: n_rows must be the strip's " +
                                        std::to_string(rows) + " tile rows");
+    GSR_TRY(order_stream(ctx, static_cast<hipStream_t>(stream)));
     GSR_HIP(gsr_launch_row_pairs(static_cast<const uint2 *>(ctx->ranges_local.p), ctx->last_gx,
                                  rows, row_pairs, static_cast<hipStream_t>(stream)),
             "row pairs launch");
@@ -1391,8 +1431,10 @@ int gsr_depth_argsort(gsr_context *ctx, const float *xyz, int64_t P, const float
     if (!ctx || P < 0 || !view_host16 || (P > 0 && (!xyz || !out_index)))
         return fail(GSR_E_INVALID, "gsr_depth_argsort: bad arguments");
     if (P > (int64_t)INT32_MAX) return fail(GSR_E_INVALID, "gsr_depth_argsort: P too large");
+    std::lock_guard<std::mutex> lock(ctx->mu);
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (P == 0) return GSR_OK;
+    GSR_TRY(order_stream(ctx, s));
     GSR_TRY(reserve_P(ctx, P, s));
     uint32_t *k = static_cast<uint32_t *>(ctx->sort_keys.p);
     GSR_HIP(gsr_launch_view_depth_keys(xyz, P, view_host16[8], view_host16[9], view_host16[10],

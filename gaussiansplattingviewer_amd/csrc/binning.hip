@@ -450,7 +450,6 @@ __global__ __launch_bounds__(kCG) void k_col_count(const uint32_t *__restrict__ 
                                                    uint4 *__restrict__ rc_sorted,
                                                    uint32_t *__restrict__ hist, int64_t ng,
                                                    uint32_t *__restrict__ off) {
-    GSR_CHAIN_ENTRY();
     __shared__ uint32_t s_diff[kCGroup][kRadixBins + 1];
     __shared__ uint32_t s_tmp[4];
     const int tid = threadIdx.x;
@@ -517,7 +516,6 @@ __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict_
                                                      const uint32_t *__restrict__ digit_total,
                                                      int pack_shift, uint32_t *__restrict__ out,
                                                      uint32_t cap, uint32_t *__restrict__ list_n) {
-    GSR_CHAIN_ENTRY();
     __shared__ ColScatterSmem c;
     __shared__ union {
         RadixTileSmem<kCW, kCIt> big;
@@ -706,10 +704,7 @@ namespace {
 //                      along the row.
 // Tiles without pairs get (0, 0), as upstream's memset leaves them.  Replaces k_ranges, a pass
 // over the K sorted keys on the main stream (the packed pair list has no tile keys to scan).
-#ifndef GSR_DIFF_THREADS
-#define GSR_DIFF_THREADS 1024
-#endif
-constexpr int kDiffThreads = GSR_DIFF_THREADS;
+constexpr int kDiffThreads = 1024;
 
 // kTight: the {rect, span word} records, column-major differences (two atomics per kept column,
 // then a prefix down each column); else the rects, row-major differences (two atomics per rect
@@ -719,7 +714,6 @@ __global__ __launch_bounds__(kDiffThreads) void k_tile_diff(const uint2 *__restr
                                                             const uint4 *__restrict__ strip_rc,
                                                             int64_t P, uint32_t gx, uint32_t rows,
                                                             uint32_t *__restrict__ partial) {
-    GSR_CHAIN_ENTRY();
     extern __shared__ uint32_t s_diff[];
     const uint32_t w1 = gx + 1, cells = gsr_tile_diff_cells(gx, rows);
     uint32_t *s_rows = s_diff + w1 * (rows + 1);  // the rows' pair totals
@@ -815,7 +809,6 @@ __global__ __launch_bounds__(kFinThreads) void k_tile_finalize(const uint32_t *_
                                                                int nparts, uint32_t gx,
                                                                uint32_t rows,
                                                                uint2 *__restrict__ ranges) {
-    GSR_CHAIN_ENTRY();
     constexpr int kW = kFinThreads / 64;
     __shared__ uint32_t s_tmp[kW];
     const uint32_t y = blockIdx.x, w1 = gx + 1, cells = gsr_tile_diff_cells(gx, rows);

@@ -73,7 +73,6 @@ __global__ __launch_bounds__(kDThreads) void k_ds_upsweep(const void *__restrict
                                                           uint32_t *__restrict__ hist,
                                                           const uint32_t *__restrict__ d_n,
                                                           int msd) {
-    GSR_CHAIN_ENTRY();
     __shared__ uint32_t s_h[kDBins];
     __shared__ uint32_t s_red[3][kDW];
     if (kFirst && msd) shift = (int)ctl[2];
@@ -173,7 +172,6 @@ __global__ __launch_bounds__(256) void k_ds_scan(uint32_t *__restrict__ hist, in
                                                  const uint32_t *__restrict__ d_n,
                                                  unsigned long long *host_D, uint32_t tag,
                                                  int msd) {
-    GSR_CHAIN_ENTRY();
     __shared__ uint32_t s_sum[kScanGroups][kScanDigits];
     __shared__ uint32_t s_red[3][4];
     if (kFirst && msd) shift = (int)ctl[2];
@@ -341,7 +339,6 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
     int64_t n_host, int drop, const uint32_t *__restrict__ ctl, int shift,
     const uint32_t *__restrict__ hist, const uint32_t *__restrict__ digit_total,
     const uint32_t *__restrict__ ids_in, const uint32_t *__restrict__ d_n, int msd) {
-    GSR_CHAIN_ENTRY();
     __shared__ uint32_t s_keys[kDT], s_vals[kDT], s_tab[kDBins];  // 48 KiB
     __shared__ uint32_t s_wcnt[kDSubBins * kDW];
     __shared__ uint32_t s_tmp[kDW];
@@ -774,7 +771,11 @@ __device__ __forceinline__ void wave_sort_bucket(const uint2 *__restrict__ src,
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-        for (int j = 0; j < kIt; ++j) {  // (the slice's slots past n: stale, never valid)
+        // Invariant: the slice's slots past n hold stale LDS data (earlier blocks' keys, whose
+        // bits 16+ may be set).  Such an item is never valid (e >= n): its digit never reaches
+        // a ballot's valid mask, cnt or a store, and the kPack rank bits OR-ed into it are never
+        // read.  Every key at a slot < n was stored masked (kj above).
+        for (int j = 0; j < kIt; ++j) {
             k[j] = s_keys[j * 64 + lane];
             v[j] = s_vals[j * 64 + lane];
         }
@@ -845,7 +846,6 @@ __global__ __launch_bounds__(kDThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     uint2 *__restrict__ pairs, uint2 *__restrict__ tmp, uint32_t *__restrict__ perm,
     const uint32_t *__restrict__ ctl, const uint32_t *__restrict__ digit_total,
     unsigned long long *__restrict__ host_crowd, uint32_t tag) {
-    GSR_CHAIN_ENTRY();
     __shared__ LocalSmem<kSlots> sm;
     // the bits below the MSD digit: the MSD pass's own shift (ctl[2]); 0 when D <= 12
     const int low = (int)ctl[2];

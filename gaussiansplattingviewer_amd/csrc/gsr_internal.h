@@ -15,15 +15,6 @@
 #define GSR_TILE_Y 16
 #define GSR_WAVE 64
 
-// Issue priority of the frame chain's waves (lab switch: build with -DGSR_CHAIN_PRIO=p, 1..3):
-// s_setprio at the entry of every kernel before the blend, so that where two frames are in
-// flight the next frame's chain waves issue ahead of the current frame's blend waves on a SIMD.
-#ifdef GSR_CHAIN_PRIO
-#define GSR_CHAIN_ENTRY() __builtin_amdgcn_s_setprio(GSR_CHAIN_PRIO)
-#else
-#define GSR_CHAIN_ENTRY() ((void)0)
-#endif
-
 namespace gsr {
 
 // One visible Gaussian as the blend consumes it: 48 B, three 16-B loads, gathered by tile
@@ -299,6 +290,8 @@ hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, hipStream_t s);
 // SH -> RGB (or colors_precomp) of every Gaussian with radii > 0 into SplatRecord.c.yzw (+ rgb).
 // waves_per_simd (1..7): cap on the colour waves a CU holds at once (0 = no cap).
 hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int waves_per_simd, hipStream_t s);
+// Once per device (gsr_create): k_color's dynamic LDS limit for those reservations.
+hipError_t gsr_color_setup();
 // Colour of the Gaussians listed in ids[0 .. *d_n) (the depth sort's compacted kept ids of a
 // strip frame), degree-3 16-B-aligned SH and no rgb output only (gsr_color_ids_ok).
 bool gsr_color_ids_ok(const GsrPreprocessArgs &a);

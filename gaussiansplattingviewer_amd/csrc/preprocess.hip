@@ -421,7 +421,6 @@ struct SkipSmem {
 // (A separate pass re-reading the rects and keys took 7 us at C3 and 42 us on a C4 strip.)
 template <bool kSkip>
 __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
-    GSR_CHAIN_ENTRY();
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t key = 0xFFFFFFFFu;
     uint32_t pairs = 0u, tight = 0u;
@@ -516,16 +515,12 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
 // memory (system scope) so the host can read them as soon as this kernel's completion event
 // fires -- no copy, and nothing added to the main stream.  host_K[0] = K, host_K[1] = D,
 // host_K[3] = the pair count over the spans (the high halves of the block counts).
-#ifndef GSR_PUBLISH_THREADS
-#define GSR_PUBLISH_THREADS 1024
-#endif
-constexpr int kPubThreads = GSR_PUBLISH_THREADS, kPubWaves = kPubThreads / 64;
+constexpr int kPubThreads = 1024, kPubWaves = kPubThreads / 64;
 __global__ __launch_bounds__(kPubThreads) void k_publish_K(const unsigned long long *__restrict__ cnt,
                                                            const uint2 *__restrict__ keybits,
                                                            int64_t n, unsigned long long *host_K,
                                                            uint32_t k_tag, uint32_t *ds_ctl,
                                                            const uint32_t *d_tag) {
-    GSR_CHAIN_ENTRY();
     __shared__ unsigned long long s_w[kPubWaves], s_wt[kPubWaves];
     __shared__ uint32_t s_max[kPubWaves], s_min[kPubWaves];
     unsigned long long v = 0, vt = 0;
@@ -649,7 +644,6 @@ __device__ __forceinline__ void store_color(const GsrPreprocessArgs &a, int64_t 
 // needed: 3,259 vs 3,400 frames/s); an LDS transpose of all 64 rows at once (144 vs 83 us); the
 // visible rows only, ranked by ballot and staged through LDS (C3 -7 %, round 5, k_color_slab).
 __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
-    GSR_CHAIN_ENTRY();
     extern __shared__ uint32_t s_occupancy_cap[];  // reserved only to cap blocks per CU
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t n_waves = (a.P + 63) / 64;
@@ -667,51 +661,6 @@ __global__ __launch_bounds__(256) void k_color(const GsrPreprocessArgs a) {
     }
     if (a.P < 0) s_occupancy_cap[threadIdx.x] = 0u;  // never: keeps the allocation referenced
 }
-
-#ifdef GSR_COLOR_SLAB
-// Lab: k_color with the rows staged through LDS.  The wave's lanes that need a colour are ranked
-// by ballot; their rows are read cooperatively -- consecutive lanes take consecutive 16-B pieces
-// of a row, so each load instruction covers ~5 whole rows (~8 full lines) instead of one piece of
-// 64 rows -- into the wave's LDS slab (64 rows of 12 float4, padded to 13), and each such lane
-// then evaluates its own row from LDS in eval_sh3_stream's order (identical colours).
-constexpr int kSlabRow = 13;  // float4 per staged row (12 + 1 pad)
-constexpr size_t kSlabBytes = 4 * 64 * (kSlabRow * 16 + 4);  // 4 waves: rows + lane map
-__global__ __launch_bounds__(256) void k_color_slab(const GsrPreprocessArgs a) {
-    GSR_CHAIN_ENTRY();
-    extern __shared__ float4 s_slab[];  // [4 waves][64][kSlabRow], then [4 waves][64] lane ids
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    float4 *slab = s_slab + w * 64 * kSlabRow;
-    int *lane_of = reinterpret_cast<int *>(s_slab + 4 * 64 * kSlabRow) + w * 64;
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    const float4 *sh = reinterpret_cast<const float4 *>(a.shs);
-    const int64_t n_waves = (a.P + 63) / 64;
-    const int64_t wave_stride = (int64_t)gridDim.x * 4;
-    for (int64_t wv = (int64_t)blockIdx.x * 4 + w; wv < n_waves; wv += wave_stride) {
-        const int64_t idx = wv * 64 + lane;
-        const bool need = idx < a.P && (a.rgb ? a.radii[idx] != 0 : a.strip_rect[idx].x != 0u);
-        const uint64_t m = __ballot(need);
-        const int nv = __popcll(m);
-        if (nv == 0) continue;
-        const int vr = __popcll(m & lt);
-        if (need) lane_of[vr] = lane;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (int q = lane; q < nv * 12; q += 64) {
-            const int r = q / 12, j = q - 12 * r;
-            slab[r * kSlabRow + j] = sh[(wv * 64 + lane_of[r]) * 12 + j];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (need) {
-            const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1],
-                                         a.means3D[3 * idx + 2]);
-            store_color(a, idx, eval_sh3_stream(p, a.campos, slab + vr * kSlabRow));
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the slab is refilled next)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-}
-#endif
 
 // The colour pass of a compacted strip frame: one lane per kept Gaussian of ids[0 .. *d_n)
 // (k_ds_compact's list), so every lane of a wave reads a row instead of ~1 in 8 on a 1/8 strip,
@@ -778,46 +727,21 @@ hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int waves_per_simd, hipS
         return hipGetLastError();
     }
     // a 4-wave block puts one wave on each SIMD: w blocks per CU = w waves per SIMD, held by
-    // reserving 1/w of the CU's 160 KiB of LDS per block (1 KiB granules)
-    size_t lds = 0;
-#ifdef GSR_COLOR_BLOCKS_PER_CU
-    // lab: cap the grid instead of reserving LDS (blocks land wherever a CU has wave slots)
-    if (waves_per_simd >= 1 && waves_per_simd < 8) {
-        const unsigned cap = 256u * GSR_COLOR_BLOCKS_PER_CU;
-        hipLaunchKernelGGL(k_color, dim3(g0 < cap ? g0 : cap), dim3(256), 0, s, a);
-        return hipGetLastError();
-    }
-#endif
-    if (waves_per_simd >= 1 && waves_per_simd < 8) {
-        lds = (size_t)(160 * 1024 / waves_per_simd) & ~(size_t)1023;
-#ifdef GSR_COLOR_LDS_MIN  // lab: the least LDS that still keeps a (w + 1)-th block out of the CU
-        lds = ((size_t)(160 * 1024 / (waves_per_simd + 1)) & ~(size_t)1023) + 1024;
-#endif
-#ifdef GSR_COLOR_SLAB
-        if (lds < kSlabBytes) lds = kSlabBytes;
-        const void *kern = reinterpret_cast<const void *>(&k_color_slab);
-#else
-        const void *kern = reinterpret_cast<const void *>(&k_color);
-#endif
-        if (lds > 64 * 1024) {
-            const hipError_t e =
-                hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
-        }
-    }
-#ifdef GSR_COLOR_SLAB
-    if (lds < kSlabBytes) {
-        lds = kSlabBytes;
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_color_slab),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 (int)lds);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(k_color_slab, dim3(g0), dim3(256), lds, s, a);
-#else
+    // reserving 1/w of the CU's 160 KiB of LDS per block (1 KiB granules; the kernel's dynamic
+    // LDS limit is raised once per device, gsr_color_setup)
+    const size_t lds = (waves_per_simd >= 1 && waves_per_simd < 8)
+                           ? (size_t)(160 * 1024 / waves_per_simd) & ~(size_t)1023
+                           : 0;
     hipLaunchKernelGGL(k_color, dim3(g0), dim3(256), lds, s, a);
-#endif
     return hipGetLastError();
+}
+
+// Raises k_color's dynamic LDS limit to the largest reservation gsr_launch_color asks for (one
+// wave per SIMD: all 160 KiB), once per device from gsr_create -- outside any stream capture, so
+// a recorded frame graph never holds a hipFuncSetAttribute.
+hipError_t gsr_color_setup() {
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(&k_color),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
 bool gsr_color_ids_ok(const GsrPreprocessArgs &a) {

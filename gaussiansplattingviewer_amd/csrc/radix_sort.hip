@@ -55,7 +55,6 @@ __global__ __launch_bounds__(kW * 64) void k_rs_upsweep(const uint32_t *__restri
                                                         uint32_t *__restrict__ hist,
                                                         int64_t stride,
                                                         const uint32_t *__restrict__ d_n) {
-    GSR_CHAIN_ENTRY();
     constexpr int kThreads = kW * 64, kT = kThreads * kIt;
     const int64_t n = live_count(d_n, n_cap);
     static_assert(kIt % 4 == 0, "full tiles are read as uint4");
@@ -107,7 +106,6 @@ __global__ __launch_bounds__(kW * 64) void k_rs_upsweep(const uint32_t *__restri
 __global__ __launch_bounds__(kBlock) void k_rs_scan(uint32_t *__restrict__ hist, int64_t stride,
                                                     uint32_t *__restrict__ digit_total,
                                                     const RsCount cnt, int64_t kT) {
-    GSR_CHAIN_ENTRY();
     __shared__ uint32_t s_tmp[4];
     const int64_t nb_act =
         cnt.d_n ? min(((int64_t)*cnt.d_n + kT - 1) / kT, cnt.n_host) : cnt.n_host;
@@ -151,7 +149,6 @@ __global__ __launch_bounds__(kW * 64) void k_rs_downsweep(
     uint32_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out, int64_t n_cap,
     int shift, int nbits, const uint32_t *__restrict__ hist,
     const uint32_t *__restrict__ digit_total, int64_t nb, const uint32_t *__restrict__ d_n) {
-    GSR_CHAIN_ENTRY();
     constexpr int kT = kW * 64 * kIt;
     const int64_t n = live_count(d_n, n_cap);
     __shared__ uint32_t s_keys[kT];

@@ -27,7 +27,7 @@ class FramePipeline:
             with pipe.frame() as slot:          # enters the frame's stream
                 res = rasterize_gaussians_native(..., slot=slot)
             ...
-        pipe.synchronize()
+        pipe.close()                            # waits; restores slot 0's options
 
     Frame i runs on stream i % depth; slot 0 is the caller's current stream, so depth=1 is the
     serial forward.  A consumer on another stream must order itself after the frame
@@ -62,15 +62,18 @@ class FramePipeline:
         # -2 %, C4 even; profiles/r05l_ab_frame_graphs.txt, r05o_ab_graphs_configs.txt), and a
         # serial frame pays ~15 us of GPU time for graph dispatch.  Images are bit-identical
         # either way (tests/test_gpu_frame_graphs.py).
+        # Slot 0 is the process-wide context the caller's own forwards (GaussianRasterizer, `_C`)
+        # render with: its two options are saved here and restored by close(), so serial callers
+        # after the pipeline get back the mode they had.
         from . import _lib
         index = dev.index if dev.index is not None else torch.cuda.current_device()
-        lib = _lib.load_library()
+        self._index = index
+        opts = (_lib.GSR_OPT_FRAME_GRAPHS, _lib.GSR_OPT_SECOND_STREAM)
+        self._slot0_saved = {o: _lib.get_option(_lib.context(index, 0), o) for o in opts}
         for slot in range(depth):
             ctx = _lib.context(index, slot)
-            _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_FRAME_GRAPHS, int(self.graphs)),
-                       "gsr_set_option")
-            _lib.check(lib.gsr_set_option(ctx, _lib.GSR_OPT_SECOND_STREAM,
-                                          int(self.second_stream)), "gsr_set_option")
+            _lib.set_option(ctx, _lib.GSR_OPT_FRAME_GRAPHS, int(self.graphs))
+            _lib.set_option(ctx, _lib.GSR_OPT_SECOND_STREAM, int(self.second_stream))
 
     def frame(self):
         """Context manager for the next frame: enters its stream, yields its context slot."""
@@ -89,6 +92,23 @@ class FramePipeline:
     def synchronize(self) -> None:
         for s in self.streams:
             s.synchronize()
+
+    def close(self) -> None:
+        """Waits for the frames in flight and restores slot 0's options (idempotent)."""
+        if self._slot0_saved is None:
+            return
+        from . import _lib
+        self.synchronize()
+        ctx = _lib.context(self._index, 0)
+        for o, v in self._slot0_saved.items():
+            _lib.set_option(ctx, o, v)
+        self._slot0_saved = None
+
+    def __enter__(self) -> "FramePipeline":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
 
 
 class _FrameScope:

@@ -29,7 +29,13 @@
  *     soon as the preprocess has counted it, while the depth sort runs.  With frame graphs
  *     (GSR_OPT_FRAME_GRAPHS) that wait comes after the whole frame is queued;
  *   - every function returns GSR_OK (0) or a negative GSR_E* code; gsr_last_error()
- *     returns the calling thread's last message.  The Python layer raises RuntimeError.
+ *     returns the calling thread's last message.  The Python layer raises RuntimeError;
+ *   - a context serves one call at a time: every entry point taking a gsr_context holds the
+ *     context's mutex for the call (two host threads rendering on one context are serialised,
+ *     not interleaved).  Its workspace is ordered on the stream of the call that used it last: a
+ *     call on another stream first waits for the device (hipDeviceSynchronize), so a context
+ *     used from two streams stays correct but serial.  Frames meant to overlap on the GPU use
+ *     one context (and one stream) each.
  */
 #ifndef GSR_H
 #define GSR_H
@@ -42,8 +48,9 @@ extern "C" {
 
 /* 2 (round 4): option ids renumbered (GSR_OPT_COLUMN_PAIRS retired, tight binning moved to 13,
  * ids 10 and 12 reserved), GSR_OPT_DEPTH_SORT (id 11, was COMPACT_SORT) gains the MSD form,
- * gsr_get_binning exports tight lists. */
-#define GSR_ABI_VERSION 2
+ * gsr_get_binning exports tight lists.
+ * 3 (round 6): gsr_get_option; contexts are serialised by a mutex and ordered across streams. */
+#define GSR_ABI_VERSION 3
 
 enum {
     GSR_OK = 0,
@@ -255,6 +262,8 @@ const char *gsr_stage_name(int i);
 enum { GSR_OPT_BLEND_CULL = 1, GSR_OPT_BLEND_FAST = 2, GSR_OPT_DEPTH_SORT = 11,
        GSR_OPT_TIGHT_BINNING = 13, GSR_OPT_FRAME_GRAPHS = 14, GSR_OPT_SECOND_STREAM = 15 };
 int gsr_set_option(gsr_context *ctx, int option, int64_t value);
+/* The current value of an option (so a caller that changes one can restore it). */
+int gsr_get_option(gsr_context *ctx, int option, int64_t *value);
 
 /* Frame-graph counters of a context: stats[0] forwards rendered by replaying graphs,
  * stats[1] graph pairs recorded, stats[2] forwards re-rendered after the list outgrew the

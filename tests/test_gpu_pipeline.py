@@ -164,3 +164,64 @@ def test_one_stream_frames_clustered_scene(gpu):
         assert k0 == k1
         assert torch.equal(r0, r1)
         assert torch.equal(c0.view(torch.int32), c1.view(torch.int32))
+
+
+def test_pipeline_close_restores_slot0_options(gpu):
+    """FramePipeline changes slot 0's frame-graph and second-stream options (slot 0 is the
+    caller's own context) and close() gives the caller back what it had."""
+    from gaussiansplattingviewer_amd import _lib
+    ctx = _lib.context(gpu.index or 0, 0)
+    _lib.set_option(ctx, _lib.GSR_OPT_SECOND_STREAM, 1)
+    _lib.set_option(ctx, _lib.GSR_OPT_FRAME_GRAPHS, 2)
+    with FramePipeline(4, gpu) as pipe:
+        assert not pipe.second_stream
+        assert _lib.get_option(ctx, _lib.GSR_OPT_SECOND_STREAM) == 0
+        assert _lib.get_option(ctx, _lib.GSR_OPT_FRAME_GRAPHS) == 0
+    assert _lib.get_option(ctx, _lib.GSR_OPT_SECOND_STREAM) == 1
+    assert _lib.get_option(ctx, _lib.GSR_OPT_FRAME_GRAPHS) == 2
+    _lib.set_option(ctx, _lib.GSR_OPT_FRAME_GRAPHS, 0)
+    for opt in (_lib.GSR_OPT_BLEND_CULL, _lib.GSR_OPT_BLEND_FAST, _lib.GSR_OPT_TIGHT_BINNING):
+        assert _lib.get_option(ctx, opt) == 1
+    assert _lib.get_option(ctx, _lib.GSR_OPT_DEPTH_SORT) == -1
+    with pytest.raises(RuntimeError, match="unknown option"):
+        _lib.get_option(ctx, 10)
+
+
+def test_threads_and_streams_share_one_context(gpu):
+    """Two host threads render through one context (slot 0) at once, each on a stream of its
+    own: the context's mutex serialises the calls and a stream switch waits for the previous
+    stream's work, so every frame equals its serial render."""
+    import threading
+    P, W, H, n = 40_000, 480, 320, 6
+    _, dg, cams = _scene(gpu, P, W, H, n, seed=23)
+    ref = []
+    for cam in cams:
+        r = _render(dg, cam, W, H, gpu)
+        ref.append((r.num_rendered, r.color.clone()))
+    torch.cuda.synchronize()
+    out = {}
+    errors = []
+
+    def worker(t):
+        try:
+            s = torch.cuda.Stream(gpu)
+            with torch.cuda.stream(s):
+                for rep in range(4):
+                    for i in range(t, n, 2):
+                        r = _render(dg, cams[i], W, H, gpu)
+                        out[(t, rep, i)] = (r.num_rendered, r.color)
+            s.synchronize()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+    assert len(out) == 4 * n
+    for (t, rep, i), (k, color) in out.items():
+        assert k == ref[i][0]
+        assert torch.equal(color.view(torch.int32), ref[i][1].view(torch.int32)), (t, rep, i)

@@ -79,7 +79,9 @@ __device__ __forceinline__ bool may_touch(float x, float y, float A, float B, fl
 // regions are spread evenly over the 8 XCDs.  With `order` (k_blend_order) the groups are
 // dealt heaviest first: every wave of the last round is then a short one, and the kernel's
 // tail -- the last waves finishing on an emptying chip -- shrinks.
-constexpr uint32_t kXcdGroup = 16;
+// work items per tile: its two 16 x 8 halves (one wave each); kXcdGroup items = 4 tiles
+constexpr uint32_t kItemsPerTile = 2;
+constexpr uint32_t kXcdGroup = 4 * kItemsPerTile;
 __device__ __forceinline__ uint32_t xcd_work(uint32_t b, const uint32_t *order,
                                              uint32_t n_groups) {
     const uint32_t x = b & 7u, l = b >> 3;
@@ -94,9 +96,9 @@ __device__ __forceinline__ uint32_t xcd_work(uint32_t b, const uint32_t *order,
 constexpr int kOrderBuckets = 1024;
 __device__ __forceinline__ uint32_t order_key(const uint2 *ranges, uint32_t g, uint32_t n_tiles) {
     uint32_t n = 0;
-    const uint32_t t0 = g * (kXcdGroup / 4u);
+    const uint32_t t0 = g * (kXcdGroup / kItemsPerTile);
 #pragma unroll
-    for (uint32_t i = 0; i < kXcdGroup / 4u; ++i)
+    for (uint32_t i = 0; i < kXcdGroup / kItemsPerTile; ++i)
         if (t0 + i < n_tiles) {
             const uint2 r = ranges[t0 + i];
             n += r.y - r.x;
@@ -166,8 +168,10 @@ struct StagedSplat {
 // blend's VALU; the extra pass over the lists cost more than it saved).
 // kContrib: track the last contributor (the n_contrib output); off (no n_contrib requested),
 // the composite step loses one v_cndmask.
+// (n_contrib: one more register per pixel; 7 waves per SIMD instead of spilling at 8)
 template <bool kFast, bool kContrib>
-__global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_t n_work) {
+__global__ __launch_bounds__(64, kContrib ? 7 : 8) void k_blend_q(const GsrBlendArgs a,
+                                                                  uint32_t n_work) {
     __shared__ StagedSplat s_spl[64];
     constexpr bool kPair = kFast && !kContrib;  // paired colour / bound words (see staging)
 
@@ -176,71 +180,79 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
     if (work >= n_work) return;
     if (a.list_n && *a.list_n > a.list_cap) return;  // not binned (frame graphs: re-rendered)
     const int lane = threadIdx.x;
-    const uint32_t tile = work >> 2, quad = work & 3u;
+    const uint32_t tile = work >> 1, half = work & 1u;
     const uint32_t tx = tile % a.grid_x, ty_local = tile / a.grid_x, ty = a.row_begin + ty_local;
-    const int qx0 = (int)tx * GSR_TILE_X + (int)(quad & 1u) * 8;
-    const int qy0 = (int)ty * GSR_TILE_Y + (int)(quad >> 1) * 8;
-    const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
-    const bool inside = px < a.W && py < a.H;
-    const float pfx = (float)px, pfy = (float)py;
-    // fast: the lane's offset from the quadrant centre and its products (exact small values)
-    const float pu = (float)(lane & 7) - 3.5f, pv = (float)(lane >> 3) - 3.5f;
-    const float puu = pu * pu, puv = pu * pv, pvv = pv * pv;
+    // the half's 16 x 8 pixels: lane (lx, ly) owns (lx, ly) of the left 8 x 8 quadrant (pixel A)
+    // and (lx + 8, ly) of the right one (pixel B)
+    const int qx0 = (int)tx * GSR_TILE_X;
+    const int qy0 = (int)ty * GSR_TILE_Y + (int)half * 8;
+    const int lx = lane & 7, ly = lane >> 3;
+    const int pxA = qx0 + lx, pxB = pxA + 8, py = qy0 + ly;
+    const bool insideA = pxA < a.W && py < a.H, insideB = pxB < a.W && py < a.H;
+    const float pfxA = (float)pxA, pfxB = (float)pxB, pfy = (float)py;
+    // fast: the pixels' offsets from the half's centre (exact small values)
+    const float uA = (float)lx - 7.5f, uB = (float)lx + 0.5f, pv = (float)ly - 3.5f;
+    const float uuA = uA * uA, uuB = uB * uB, pvv = pv * pv;
 
     const uint2 range = a.ranges[tile];
-    // done carried in the sign of T, as in k_blend
-    float T = inside ? 1.0f : -1.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f;
-    uint32_t last_contributor = 0;
-    auto live_any = [&]() { return __ballot(!(T <= 0.0f)) != 0ull; };
+    // done carried in the sign of T
+    float TA = insideA ? 1.0f : -1.0f, TB = insideB ? 1.0f : -1.0f;
+    float A0 = 0.0f, A1 = 0.0f, A2 = 0.0f, B0 = 0.0f, B1 = 0.0f, B2 = 0.0f;
+    uint32_t lastA = 0, lastB = 0;
+    auto live_any = [&]() { return __ballot(!(TA <= 0.0f) || !(TB <= 0.0f)) != 0ull; };
     if (!live_any()) return;
 
-    // kBound (fast form): test upstream's power > 0 skip as p > bound -- only chunks holding a
-    // conic that is not positive definite need it (staging below)
-    auto composite = [&](const StagedSplat &sp, auto bound_tag) {
+    // one pixel's update from its exponent p (fast form)
+    auto update_fast = [&](float p, float bound, float cr, float cg, float cb, uint32_t pos,
+                           float &T, float &C0, float &C1, float &C2, uint32_t &last,
+                           auto bound_tag) {
         constexpr bool kBound = decltype(bound_tag)::value;
-        bool vis, acc, term;
-        float test_T;
-        if (kFast) {
-            // The loop-carried chain is only T -> T (1 - alpha_eff) -> compare -> select:
-            // alpha_eff = 0 for an invisible splat (then test_T = T), and a pixel that
-            // terminates keeps -|T| (idempotent once done).  The weight is |T| - |T'|: T - test_T
-            // while the pixel composites, 0 for the terminating splat and after it.
-            float p2 = __builtin_fmaf(sp.g.y, pu, sp.g.x);
-            p2 = __builtin_fmaf(sp.g.z, pv, p2);
-            p2 = __builtin_fmaf(sp.g.w, puu, p2);
-            p2 = __builtin_fmaf(sp.q.x, puv, p2);
-            p2 = __builtin_fmaf(sp.q.y, pvv, p2);
-            const float alpha = fminf(0.99f, __builtin_amdgcn_exp2f(p2));
-            vis = !(alpha < 1.0f / 255.0f);
-            if (kBound) vis = vis && !(p2 > sp.e.z);
-            // T (1 - alpha) as one fma, T - alpha T; alpha_eff = 0 leaves T exactly
-            const float alpha_eff = vis ? alpha : 0.0f;
-            test_T = __builtin_fmaf(-T, alpha_eff, T);
-            const bool lo = test_T < 0.0001f;
-            const float T_next = lo ? -fabsf(T) : test_T;
-            const float wgt = fabsf(T) - fabsf(T_next);
-            C0 = __builtin_fmaf(sp.q.z, wgt, C0);
-            C1 = __builtin_fmaf(sp.q.w, wgt, C1);
-            C2 = __builtin_fmaf(sp.e.x, wgt, C2);
-            if (kContrib)
-                last_contributor = (vis && !lo) ? __float_as_uint(sp.e.y) : last_contributor;
-            T = T_next;
-            return;
-        } else {
-            const float dx = sp.g.x - pfx, dy = sp.g.y - pfy;
-            const float power =
-                -0.5f * (sp.g.z * dx * dx + sp.q.x * dy * dy) - sp.g.w * dx * dy;
-            const float alpha = fminf(0.99f, sp.q.y * exp_core(power));
-            vis = !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-            test_T = T * (1 - alpha);
-            acc = vis && !(test_T < 0.0001f);
-            term = vis && (test_T < 0.0001f);
-            C0 = acc ? C0 + sp.q.z * alpha * T : C0;
-            C1 = acc ? C1 + sp.q.w * alpha * T : C1;
-            C2 = acc ? C2 + sp.e.x * alpha * T : C2;
-        }
+        const float alpha = fminf(0.99f, __builtin_amdgcn_exp2f(p));
+        bool vis = !(alpha < 1.0f / 255.0f);
+        if (kBound) vis = vis && !(p > bound);
+        // T (1 - alpha) as one fma; alpha_eff = 0 leaves T exactly; a pixel that terminates
+        // keeps -|T|; the weight is |T| - |T'|
+        const float alpha_eff = vis ? alpha : 0.0f;
+        const float test_T = __builtin_fmaf(-T, alpha_eff, T);
+        const bool lo = test_T < 0.0001f;
+        const float T_next = lo ? -fabsf(T) : test_T;
+        const float wgt = fabsf(T) - fabsf(T_next);
+        C0 = __builtin_fmaf(cr, wgt, C0);
+        C1 = __builtin_fmaf(cg, wgt, C1);
+        C2 = __builtin_fmaf(cb, wgt, C2);
+        if (kContrib) last = (vis && !lo) ? pos : last;
+        T = T_next;
+    };
+    auto update_exact = [&](const StagedSplat &sp, float pfx, float &T, float &C0, float &C1,
+                            float &C2, uint32_t &last) {
+        const float dx = sp.g.x - pfx, dy = sp.g.y - pfy;
+        const float power = -0.5f * (sp.g.z * dx * dx + sp.q.x * dy * dy) - sp.g.w * dx * dy;
+        const float alpha = fminf(0.99f, sp.q.y * exp_core(power));
+        const bool vis = !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+        const float test_T = T * (1 - alpha);
+        const bool acc = vis && !(test_T < 0.0001f);
+        const bool term = vis && (test_T < 0.0001f);
+        C0 = acc ? C0 + sp.q.z * alpha * T : C0;
+        C1 = acc ? C1 + sp.q.w * alpha * T : C1;
+        C2 = acc ? C2 + sp.e.x * alpha * T : C2;
         T = acc ? test_T : (term ? -fabsf(T) : T);
-        if (kContrib) last_contributor = acc ? __float_as_uint(sp.e.y) : last_contributor;
+        if (kContrib) last = acc ? __float_as_uint(sp.e.y) : last;
+    };
+    // one staged splat over the lane's two pixels; fast: p = k0 + k2 v + k5 v^2 (shared) +
+    // u (k1 + k4 v) (shared factor) + k3 u^2
+    auto composite = [&](const StagedSplat &sp, auto bound_tag) {
+        if (kFast) {
+            const float base = __builtin_fmaf(sp.q.y, pvv, __builtin_fmaf(sp.g.z, pv, sp.g.x));
+            const float lin = __builtin_fmaf(sp.q.x, pv, sp.g.y);
+            const float pA = __builtin_fmaf(sp.g.w, uuA, __builtin_fmaf(lin, uA, base));
+            const float pB = __builtin_fmaf(sp.g.w, uuB, __builtin_fmaf(lin, uB, base));
+            const uint32_t pos = __float_as_uint(sp.e.y);
+            update_fast(pA, sp.e.z, sp.q.z, sp.q.w, sp.e.x, pos, TA, A0, A1, A2, lastA, bound_tag);
+            update_fast(pB, sp.e.z, sp.q.z, sp.q.w, sp.e.x, pos, TB, B0, B1, B2, lastB, bound_tag);
+        } else {
+            update_exact(sp, pfxA, TA, A0, A1, A2, lastA);
+            update_exact(sp, pfxB, TB, B0, B1, B2, lastB);
+        }
     };
     const float X0 = (float)qx0, Y0 = (float)qy0;
 
@@ -257,26 +269,23 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
         bool keep = valid;
         if (valid && a.cull)
             keep = may_touch(r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.z, r.b.w, 2.0f * r.c.x, X0,
-                             X0 + 7, Y0, Y0 + 7);
+                             X0 + 15, Y0, Y0 + 7);
         const uint64_t bal = __ballot(keep);
         bool npd = false;  // a staged conic that is not positive definite (fast form)
         if (keep) {
             StagedSplat st;
             if (kFast) {
                 // exponent log2(e) * (-q/2) = a dx^2 + b dx dy + c dy^2 with dx = ex - u,
-                // dy = ey - v, expanded in (u, v)
+                // dy = ey - v, expanded in (u, v) about the half's centre
                 const float kL2e = 1.4426950408889634f;
                 const float ca = r.a.z * (-0.5f * kL2e), cb = r.a.w * (-kL2e),
                             cc = r.b.x * (-0.5f * kL2e);
-                const float ex = r.a.x - (X0 + 3.5f), ey = r.a.y - (Y0 + 3.5f);
+                const float ex = r.a.x - (X0 + 7.5f), ey = r.a.y - (Y0 + 3.5f);
                 const float lo = __builtin_amdgcn_logf(r.b.y);  // log2(opacity)
                 const float k0 = __builtin_fmaf(ex, __builtin_fmaf(ca, ex, cb * ey), cc * ey * ey);
                 st.g = make_float4(k0 + lo, __builtin_fmaf(-2.0f * ca, ex, -cb * ey),
                                    __builtin_fmaf(-cb, ex, -2.0f * cc * ey), ca);
                 st.q = make_float4(cb, cc, r.c.y, r.c.z);
-                // upstream skips power > 0, which a positive-definite conic reaches only through
-                // rounding; the expanded form rounds differently (at a centre that falls on a
-                // pixel it can land just above 0), so the test is kept for the other conics only
                 const bool pd = ca < 0.0f && cc < 0.0f && 4.0f * ca * cc > cb * cb;
                 npd = !pd;
                 st.e = make_float4(r.c.w, __uint_as_float(idx - range.x + 1u),
@@ -289,8 +298,6 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
             const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
             const int slot = __popcll(bal & lt);  // compacted in list order
             if (kPair) {
-                // a pair's blues and power bounds share the even slot's e: {b0, b1, bound0,
-                // bound1} (5 LDS reads per composited pair instead of 6)
                 s_spl[slot].g = st.g;
                 s_spl[slot].q = st.q;
                 float *pe = &s_spl[slot & ~1].e.x;
@@ -302,9 +309,6 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
         }
         int count = __popcll(bal);
         if (count == 0) continue;
-        // the compacted slots are the list (no index indirection); an odd count is padded with
-        // an opacity-0 splat in slot `count` (< 64 for an odd count): exact: opacity 0; fast:
-        // exponent -inf (alpha 0, the bound-free loop included) and a power bound of -inf
         if (count & 1) {
             if (kPair) {
                 if (lane < 8)
@@ -318,10 +322,6 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
             }
             ++count;
         }
-        // one wave: its LDS writes above complete before the reads below are served
-
-        // single-buffered: a software-pipelined form (the next pair's LDS reads in flight
-        // during this pair) spilled past 64 VGPRs and was slower
         auto composite_all = [&](auto bound_tag) {
             for (int k = 0; k < count; k += 2) {
                 if (kPair) {
@@ -338,7 +338,6 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
                 }
             }
         };
-        // (the exact form always tests power > 0, as upstream writes it)
         if (!kFast || __ballot(npd) != 0ull)
             composite_all(std::integral_constant<bool, true>{});
         else
@@ -346,16 +345,25 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
         if (!live_any()) break;
     }
 
-    if (inside) {
-        const int row = py - a.y0;
-        const size_t pid = (size_t)row * a.W + px;
-        const size_t plane = (size_t)a.rows_out * a.W;
-        const float Tf = fabsf(T);
+    const size_t plane = (size_t)a.rows_out * a.W;
+    const size_t row = (size_t)(py - a.y0) * a.W;
+    if (insideA) {
+        const size_t pid = row + pxA;
+        const float Tf = fabsf(TA);
         if (a.final_T) a.final_T[pid] = Tf;
-        if (kContrib && a.n_contrib) a.n_contrib[pid] = last_contributor;
-        a.out_color[pid] = C0 + Tf * a.bg[0];
-        a.out_color[plane + pid] = C1 + Tf * a.bg[1];
-        a.out_color[2 * plane + pid] = C2 + Tf * a.bg[2];
+        if (kContrib && a.n_contrib) a.n_contrib[pid] = lastA;
+        a.out_color[pid] = A0 + Tf * a.bg[0];
+        a.out_color[plane + pid] = A1 + Tf * a.bg[1];
+        a.out_color[2 * plane + pid] = A2 + Tf * a.bg[2];
+    }
+    if (insideB) {
+        const size_t pid = row + pxB;
+        const float Tf = fabsf(TB);
+        if (a.final_T) a.final_T[pid] = Tf;
+        if (kContrib && a.n_contrib) a.n_contrib[pid] = lastB;
+        a.out_color[pid] = B0 + Tf * a.bg[0];
+        a.out_color[plane + pid] = B1 + Tf * a.bg[1];
+        a.out_color[2 * plane + pid] = B2 + Tf * a.bg[2];
     }
 }
 
@@ -368,7 +376,7 @@ inline uint32_t xcd_grid(uint32_t n_work) {
 }  // namespace
 
 uint32_t gsr_blend_order_groups(uint32_t n_tiles) {
-    return (4u * n_tiles + kXcdGroup - 1) / kXcdGroup;
+    return (kItemsPerTile * n_tiles + kXcdGroup - 1) / kXcdGroup;
 }
 
 hipError_t gsr_launch_blend_order(const uint2 *ranges, uint32_t n_tiles, uint32_t *order,
@@ -381,7 +389,7 @@ hipError_t gsr_launch_blend_order(const uint2 *ranges, uint32_t n_tiles, uint32_
 
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s) {
     if (a.rows_tiles == 0 || a.grid_x == 0) return hipSuccess;
-    const uint32_t n_work = 4u * a.grid_x * a.rows_tiles;
+    const uint32_t n_work = kItemsPerTile * a.grid_x * a.rows_tiles;
     const dim3 grid(xcd_grid(n_work));
     if (a.fast && !a.n_contrib)
         hipLaunchKernelGGL((k_blend_q<true, false>), grid, dim3(64), 0, s, a, n_work);

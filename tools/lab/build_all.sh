@@ -1,5 +1,5 @@
 #!/bin/bash
-# Lab builds of the whole library with extra compile flags (lab switches, e.g. -DGSR_CHAIN_PRIO=2):
+# Lab builds of the whole library with extra compile flags (experiment-only -D switches of a lab source):
 # gaussiansplattingviewer_amd/libgsr_lab_<name>.so; bench / tests pick it with GSR_LIB=<path>.
 # Usage: tools/lab/build_all.sh <name> <flags...>
 set -e
