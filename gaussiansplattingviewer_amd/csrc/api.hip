@@ -822,9 +822,12 @@ void finish_frame(gsr_context *ctx, const Frame &f, gsr_outputs *out) {
 // column-first binning, a known capacity, no debug, no per-stage timing, no
 // compaction (its colour pass waits on a mid-chain event of the frame stream), no rgb output
 // (the colour pass's).
+// (Mode 2 also runs one-stream frames: the second stream's chain then runs in order on the
+// frame's stream, as the direct path's one-stream frames do.)
 bool graph_eligible(const gsr_context *ctx, const Frame &f, const gsr_outputs *out) {
-    return ctx->graphs && ctx->second_stream && ctx->list_cap > 0 && f.colpairs && !f.dbg &&
-           f.tmode != 1 && !f.compact_sort && !f.color_ids && !out->rgb && f.P > 0;
+    return ctx->graphs && (ctx->second_stream || ctx->graphs == 2) && ctx->list_cap > 0 &&
+           f.colpairs && !f.dbg && f.tmode != 1 && !f.compact_sort && !f.color_ids && !out->rgb &&
+           f.P > 0;
 }
 
 GraphKey graph_key(const gsr_context *ctx, const Frame &f) {
@@ -1024,10 +1027,11 @@ int forward_graph(gsr_context *ctx, Frame &f, const gsr_raster_settings *st, gsr
     GSR_HIP(hipEventRecord(ctx->fork, s), "hipEventRecord(fork)");
     if (replay) GSR_HIP(hipGraphLaunch(e->sort, s), "hipGraphLaunch(depth sort)");
     else GSR_TRY(chain_sort(ctx, g, s));
-    GSR_HIP(hipStreamWaitEvent(ctx->aux, ctx->fork, 0), "hipStreamWaitEvent(fork)");
+    const bool two = ctx->second_stream != 0;  // (else mode 2 on one stream: in order on s)
+    if (two) GSR_HIP(hipStreamWaitEvent(ctx->aux, ctx->fork, 0), "hipStreamWaitEvent(fork)");
     if (replay) GSR_HIP(hipGraphLaunch(e->aux, ctx->aux), "hipGraphLaunch(second stream)");
-    else GSR_TRY(aux_chain(ctx, g, ctx->aux, fw));
-    GSR_HIP(hipEventRecord(ctx->join, ctx->aux), "hipEventRecord(join)");
+    else GSR_TRY(aux_chain(ctx, g, two ? ctx->aux : s, fw));
+    if (two) GSR_HIP(hipEventRecord(ctx->join, ctx->aux), "hipEventRecord(join)");
     uint32_t *point_list = nullptr;
     if (replay) {
         GSR_HIP(hipGraphLaunch(e->bin, s), "hipGraphLaunch(binning)");
@@ -1035,7 +1039,7 @@ int forward_graph(gsr_context *ctx, Frame &f, const gsr_raster_settings *st, gsr
     } else {
         GSR_TRY(chain_bin(ctx, g, s, &point_list));
     }
-    GSR_HIP(hipStreamWaitEvent(s, ctx->join, 0), "hipStreamWaitEvent(join)");
+    if (two) GSR_HIP(hipStreamWaitEvent(s, ctx->join, 0), "hipStreamWaitEvent(join)");
     GSR_TRY(stage_end(ctx, f, 5));
     f.point_list = point_list;
     f.tiles_local = nullptr;
@@ -1047,7 +1051,7 @@ int forward_graph(gsr_context *ctx, Frame &f, const gsr_raster_settings *st, gsr
     // host has queued the rest of the frame
     uint64_t tagv = 0;
     if (!spin_on(&ctx->h_total[7], [&](uint64_t v) { return v == f.tag; }, tagv))
-        GSR_HIP(hipStreamSynchronize(f.main_publish ? s : ctx->aux),
+        GSR_HIP(hipStreamSynchronize(f.main_publish || !two ? s : ctx->aux),
                 "hipStreamSynchronize(pair count)");
     f.K = __atomic_load_n(&ctx->h_total[2], __ATOMIC_ACQUIRE);
     ctx->last_Dr = (uint32_t)__atomic_load_n(&ctx->h_total[6], __ATOMIC_ACQUIRE);

@@ -23,11 +23,16 @@ _next_slot = [20]
 
 def _slots(dev, mode=1):
     """A fresh (graphs on, graphs off) pair of context slots; mode 1 replays recorded graphs, 2
-    launches the same deferred-K chains directly."""
+    launches the same deferred-K chains directly, "2-one-stream" does that on a context without
+    its second stream (the second stream's chain in order on the frame's stream, as four frames
+    in flight run)."""
     on, off = _next_slot[0], _next_slot[0] + 1
     _next_slot[0] += 2
-    set_option(dev, _lib.GSR_OPT_FRAME_GRAPHS, mode, on)
+    one = mode == "2-one-stream"
+    set_option(dev, _lib.GSR_OPT_FRAME_GRAPHS, 2 if one else mode, on)
     set_option(dev, _lib.GSR_OPT_FRAME_GRAPHS, 0, off)
+    set_option(dev, _lib.GSR_OPT_SECOND_STREAM, 0 if one else 1, on)
+    set_option(dev, _lib.GSR_OPT_SECOND_STREAM, 0 if one else 1, off)
     return on, off
 
 
@@ -75,7 +80,7 @@ CASES = {
 }
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, "2-one-stream"])
 @pytest.mark.parametrize("case", sorted(CASES))
 def test_graph_frames_equal_direct(gpu, case, mode):
     build, W, H, tile_rows, radii = CASES[case]
@@ -110,7 +115,7 @@ def test_graph_frames_precomputed_colours(gpu):
     assert _lib.frame_graph_stats(0, on)["graph_frames"] >= 3
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, "2-one-stream"])
 def test_graph_overflow_rerenders(gpu, mode):
     """A small scene sets the capacity; a much larger one on the same context overflows it on
     its first frame (rendered again the direct way, identical), then runs on graphs again."""
@@ -150,3 +155,29 @@ def test_graph_rerecords_on_new_inputs(gpu):
         torch.cuda.synchronize()
         _same(a, b)
     assert _lib.frame_graph_stats(0, on)["graphs_recorded"] == rec0 + 1
+
+
+def test_one_stream_deferred_k_overflow_at_c3_size(gpu):
+    """Four-frames-in-flight regime (one stream, deferred K, GSR_OPT_FRAME_GRAPHS 2) at the
+    headline size: a 100k scene sets the capacity, the C3 scene (1M Gaussians, 1920x1080,
+    ~5.8M list entries) overflows it on its first frame and is rendered again the direct way;
+    every C3 frame equals the direct forward."""
+    W, H = 1920, 1080
+    small = _scene(gpu, synthetic_gaussians(100_000, 3, 1), 3)
+    c3 = _scene(gpu, synthetic_gaussians(1_000_000, 3, 2), 3)
+    on, off = _slots(gpu, "2-one-stream")
+    cams = _cams(gpu, W, H, 5, step=3)
+    for cam in cams[:2]:
+        _render(gpu, small, cam, W, H, on)
+    torch.cuda.synchronize()
+    cap0 = _lib.frame_graph_stats(0, on)["list_cap"]
+    for cam in cams[2:]:
+        a = _render(gpu, c3, cam, W, H, on)
+        b = _render(gpu, c3, cam, W, H, off)
+        torch.cuda.synchronize()
+        _same(a, b)
+    st = _lib.frame_graph_stats(0, on)
+    assert st["overflows"] == 1 and st["list_cap"] > cap0 > 0
+    la, lb = binning_state(0, on), binning_state(0, off)
+    for x, y in zip(la, lb):
+        assert torch.equal(x, y)
