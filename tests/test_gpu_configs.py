@@ -51,28 +51,37 @@ def _collect(res, dev, slot):
     return out
 
 
-def test_c5_orbit_frames_through_pipeline(gpu, oracle_mod, c5_scene):
+@pytest.mark.parametrize("depth", [2, 4])
+def test_c5_orbit_frames_through_pipeline(gpu, oracle_mod, c5_scene, depth):
+    """C5 frames through FramePipeline: depth 4 is the bench's timed mode (four frames in
+    flight, one stream each).  Each frame is rendered twice on its slot: as the viewer calls it
+    (no per-Gaussian extras: tight binning, the paired-slot blend) and with every extra, which
+    is checked against the oracle; the viewer call's image is bit-identical to the extras
+    call's and within the image tolerance of the oracle's."""
     g = c5_scene
     P = len(g.xyz)
     dg = dict(xyz=to_dev(g.xyz, gpu), rot=to_dev(g.rot, gpu), scale=to_dev(g.scale, gpu),
               opacity=to_dev(g.opacity, gpu),
               sh=to_dev(g.sh, gpu).reshape(P, -1, 3).contiguous())
-    pipe = FramePipeline(2, gpu)
     Ks = []
-    for i in C5_FRAMES:
-        s = scene_inputs(g, static_camera(1920, 1080, orbit_eye(i, 1000)), 3)
-        with pipe.frame() as slot:
-            res = rasterize_gaussians_native(
-                to_dev(s["bg"], gpu), dg["xyz"], None, dg["opacity"], dg["scale"], dg["rot"],
-                1.0, None, to_dev(s["view"], gpu), to_dev(s["proj"], gpu), s["tx"], s["ty"],
-                s["H"], s["W"], dg["sh"], 3, to_dev(s["campos"], gpu), False, False, slot=slot,
-                extras=ALL_EXTRAS)
-            hip = _collect(res, gpu, slot)
-        orc = run_oracle(oracle_mod, s)
-        assert orc["num_rendered"] > 5_000_000, (i, orc["num_rendered"])
-        assert_parity(hip, orc)
-        Ks.append(hip["num_rendered"])
-    pipe.synchronize()
+    with FramePipeline(depth, gpu) as pipe:
+        assert pipe.second_stream == (depth < 3)
+        for i in C5_FRAMES:
+            s = scene_inputs(g, static_camera(1920, 1080, orbit_eye(i, 1000)), 3)
+            args = (to_dev(s["bg"], gpu), dg["xyz"], None, dg["opacity"], dg["scale"], dg["rot"],
+                    1.0, None, to_dev(s["view"], gpu), to_dev(s["proj"], gpu), s["tx"], s["ty"],
+                    s["H"], s["W"], dg["sh"], 3, to_dev(s["campos"], gpu), False, False)
+            with pipe.frame() as slot:
+                viewer = rasterize_gaussians_native(*args, slot=slot)
+                res = rasterize_gaussians_native(*args, slot=slot, extras=ALL_EXTRAS)
+                hip = _collect(res, gpu, slot)
+            orc = run_oracle(oracle_mod, s)
+            assert orc["num_rendered"] > 5_000_000, (i, orc["num_rendered"])
+            assert_parity(hip, orc)
+            assert viewer.num_rendered == hip["num_rendered"]
+            np.testing.assert_array_equal(viewer.color.cpu().numpy().view(np.uint32),
+                                          hip["color"].view(np.uint32))
+            Ks.append(hip["num_rendered"])
     assert len(set(Ks)) == len(Ks)  # the camera really moved (different binning per frame)
 
 
