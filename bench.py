@@ -44,8 +44,8 @@ from gaussiansplattingviewer_amd.gaussian_data import clustered_scene, synthetic
 from gaussiansplattingviewer_amd.rasterizer import (rasterize_gaussians_native, tile_row_pairs,  # noqa: E402
                                                     world_bound)
 from gaussiansplattingviewer_amd.pipeline import FramePipeline  # noqa: E402
-from gaussiansplattingviewer_amd.strips import (StripBalancer, StripGather, strip_pixel_rows,  # noqa: E402
-                                                strip_rows)
+from gaussiansplattingviewer_amd.strips import (StripBalancer, StripGather, rank_stream_plan,  # noqa: E402
+                                                strip_pixel_rows, strip_rows)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 
@@ -408,6 +408,16 @@ def main():
     # decision 12); full frames keep direct launches
     strip_graphs = args.inflight >= 2 and (world > 1 or bool(args.sim_strip))
     pipe = None  # (created below: after the serial passes on one GPU)
+    if world > 1:
+        # RCCL's communicators (and their streams) first: one all-reduce and one gather of an
+        # empty frame, so RCCL's streams exist before the frame streams are created and used
+        # (a stream's hardware queue is fixed when it is first used)
+        warm = torch.zeros((gy,), dtype=torch.int32, device=dev)
+        dist.all_reduce(warm)
+        gather.submit(gather.next_buffer(strip_pixel_rows(balancer.current[rank], H)[1]),
+                      balancer.current)
+        gather.finish()
+        torch.cuda.synchronize()
 
     def step(i):
         with pipe.frame() as slot:
@@ -628,6 +638,16 @@ def main():
                          "(each event adds a few us); the timed region records no events",
         "inflight": args.inflight,
         "second_stream": pipe.second_stream,
+        "streams": {"plan": rank_stream_plan(args.inflight, pipe.second_stream),
+                    "priority": "normal (all)",
+                    "order": ("the caller's stream and slot 0's second stream in the serial "
+                              "passes (that second stream destroyed before the pipeline at "
+                              "depth >= 3), then FramePipeline's streams in slot order, first "
+                              "used by the in-flight pass" if world == 1 else
+                              "RCCL's communicators (warm-up all-reduce + gather), then the "
+                              "FramePipeline streams in slot order"),
+                    "note": "HIP fixes a stream's hardware queue (GPU_MAX_HW_QUEUES = 4) when "
+                            "the stream is first used; the plan stays within 4 streams"},
         "timed_after": ("194 serial (64 untimed, 100 for the serial rate, 30 with stage events) "
                         "then 64 in-flight (blend events) untimed diagnostic frames, then the W "
                         "warmup frames" if world == 1 else

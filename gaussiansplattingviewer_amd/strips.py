@@ -85,7 +85,6 @@ class StripBalancer:
         self.current = strip_layout(grid_y, world)
         self.pending = None  # (apply_at, work, vec, host, event)
         self.history = []    # (frame, layout) of every change (diagnostics)
-        self._side = None    # the one stream the counts' device -> host copies run on
 
     def layout(self, frame: int) -> list[tuple[int, int]]:
         p = self.pending
@@ -106,6 +105,10 @@ class StripBalancer:
         return self.layout(frame)[self.rank]
 
     def observe(self, frame: int, row_pairs: torch.Tensor) -> None:
+        """Call on the frame's own stream (as bench.py does, inside the FramePipeline frame):
+        the counts' device -> host copy is queued there behind the all-reduce, so the balancer
+        takes no stream (and no hardware queue) of its own; that stream waits for the
+        all-reduce once every `every` frames."""
         if self.world == 1 or frame % self.every != 0 or self.pending is not None:
             return
         b, e = self.current[self.rank]
@@ -115,21 +118,26 @@ class StripBalancer:
         vec[b:e].copy_(row_pairs)
         work = dist.all_reduce(vec, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         if vec.is_cuda:
-            # one side stream for the run (a new stream per observation would take another of
-            # torch's pooled streams each time, spreading work over more hardware queues)
-            if self._side is None:
-                self._side = torch.cuda.Stream(device=vec.device)
-            side = self._side
             host = torch.empty((self.gy,), dtype=torch.int32, pin_memory=True)
-            with torch.cuda.stream(side):
-                work.wait()  # the side stream waits for the all-reduce
-                host.copy_(vec, non_blocking=True)
-                event = torch.cuda.Event()
-                event.record(side)
-            vec.record_stream(side)
+            work.wait()  # the current (frame) stream waits for the all-reduce
+            host.copy_(vec, non_blocking=True)
+            event = torch.cuda.Event()
+            event.record()
             self.pending = (frame + self.lag, work, vec, host, event)
         else:
             self.pending = (frame + self.lag, work, vec, None, None)
+
+
+def rank_stream_plan(inflight: int, second_stream: bool) -> list[str]:
+    """The HIP streams one rank's frame loop uses (bench.py): the caller's stream
+    and inflight - 1 FramePipeline streams, plus each in-flight context's second stream when on.
+    StripBalancer and StripGather create none (RCCL's collectives run on RCCL's own streams,
+    created with the communicator before these).  With GPU_MAX_HW_QUEUES = 4 the plan must stay
+    within 4 for every frame stream to have a hardware queue of its own."""
+    plan = ["caller"] + [f"frame{i}" for i in range(1, inflight)]
+    if second_stream:
+        plan += [f"second{i}" for i in range(inflight)]
+    return plan
 
 
 class StripGather:

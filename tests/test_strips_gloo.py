@@ -181,3 +181,56 @@ def test_balanced_layout_properties(seed):
     loads = [int(c[b:e].sum()) for b, e in lay]
     if c.sum() > 0 and gy >= world:
         assert max(loads) <= c.sum() / world + c.max() * 2
+
+
+def _stream_count_worker(rank, world, port, gy, gx, H, W, result_path):
+    """A strip rank's bench loop without the renderer (gloo): StripBalancer + StripGather over
+    13 frames, with torch.cuda.Stream counted -- they must create none."""
+    from gaussiansplattingviewer_amd import strips
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    created = []
+    real = torch.cuda.Stream
+
+    class Counting:
+        def __new__(cls, *a, **k):
+            created.append(1)
+            return real(*a, **k)
+
+    torch.cuda.Stream = Counting
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        bal = strips.StripBalancer(gy, gx, world, rank, every=4, lag=2)
+        gat = strips.StripGather(H, W, world, rank, depth=3)
+        for f in range(13):
+            if len(gat.pending) == len(gat.slots) - 1:
+                gat.finish()
+            lay = bal.layout(f)
+            b, e = lay[rank]
+            buf = gat.next_buffer(strips.strip_pixel_rows(lay[rank], H)[1])
+            buf.fill_(float(rank))
+            gat.submit(buf, lay)
+            bal.observe(f, torch.full((e - b,), 10 + rank, dtype=torch.int32))
+        while gat.pending:
+            gat.finish()
+        np.save(result_path + f".{rank}.npy", np.array([len(created)]))
+    finally:
+        torch.cuda.Stream = real
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_strip_rank_stream_budget(tmp_path, world):
+    """The queue budget of a strip rank: the balancer and the gather create no
+    streams of their own, and the bench's strip plan (two frames in flight, each with its
+    second stream) uses exactly GPU_MAX_HW_QUEUES = 4 streams; four one-stream frames too."""
+    from gaussiansplattingviewer_amd.strips import rank_stream_plan
+    gy, gx, H, W = 20, 12, 320, 192
+    rp = str(tmp_path / "streams")
+    mp.start_processes(_stream_count_worker, args=(world, _free_port(), gy, gx, H, W, rp),
+                       nprocs=world, join=True, start_method="spawn")
+    for r in range(world):
+        assert int(np.load(rp + f".{r}.npy")[0]) == 0
+    assert len(rank_stream_plan(2, True)) == 4
+    assert len(rank_stream_plan(4, False)) == 4
+    assert len(rank_stream_plan(3, True)) > 4  # (the combination the bench avoids)
