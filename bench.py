@@ -41,8 +41,7 @@ sys.path.insert(0, REPO)
 from gaussiansplattingviewer_amd import _lib  # noqa: E402
 from gaussiansplattingviewer_amd.camera import cuda_camera_inputs, orbit_eye, static_camera  # noqa: E402
 from gaussiansplattingviewer_amd.gaussian_data import clustered_scene, synthetic_gaussians  # noqa: E402
-from gaussiansplattingviewer_amd.rasterizer import (rasterize_gaussians_native, tile_row_pairs,  # noqa: E402
-                                                    world_bound)
+from gaussiansplattingviewer_amd.rasterizer import rasterize_gaussians_native, tile_row_pairs  # noqa: E402
 from gaussiansplattingviewer_amd.pipeline import FramePipeline  # noqa: E402
 from gaussiansplattingviewer_amd.strips import (StripBalancer, StripGather, rank_stream_plan,  # noqa: E402
                                                 strip_pixel_rows, strip_rows)
@@ -94,9 +93,6 @@ def parse():
     ap.add_argument("--second-stream", type=int, default=None, choices=[0, 1],
                     help="GSR_OPT_SECOND_STREAM of the in-flight frames (default: FramePipeline's "
                          "choice -- off at depth >= 3 without frame graphs)")
-    ap.add_argument("--bound", type=int, default=1, choices=[0, 1],
-                    help="strip frames: pass the per-scene world-space bound (gsr_world_bound, "
-                         "computed once at upload) so the reach test reads xyz + the bound")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU-oracle time to sample for cpu_baseline (whole frames; at least one)")
     return ap.parse_args()
@@ -113,9 +109,6 @@ class Scene:
         up = lambda a: torch.as_tensor(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         self.xyz, self.rot, self.scale, self.opacity = up(g.xyz), up(g.rot), up(g.scale), up(g.opacity)
         self.sh = up(g.sh).reshape(P, -1, 3).contiguous()
-        # the per-scene bound strip frames reach with (the viewer's load-time hook)
-        self.bound = world_bound(self.scale, self.rot)
-        self.use_bound = True
         self.bg = torch.zeros(3, device=dev)
         self.dev = dev
         self.cams = []
@@ -134,7 +127,7 @@ class Scene:
                                           self.rot, 1.0, None, view, proj, tx, ty, self.H, self.W,
                                           self.sh, self.deg, campos, False, False,
                                           tile_rows=tile_rows, slot=slot, out_color=out_color,
-                                          radii=radii, bound3D=self.bound if self.use_bound else None)
+                                          radii=radii)
 
 
 # Committed rocprofv3 profiles (tools/profile_config.sh on the GPU box, summarised here by
@@ -383,7 +376,6 @@ def main():
                                 device_id=torch.device("cuda", local))
 
     scene = Scene(args.config, dev)
-    scene.use_bound = bool(args.bound)
     W, H = scene.W, scene.H
     gy, gx = (H + 15) // 16, (W + 15) // 16
     rows = None

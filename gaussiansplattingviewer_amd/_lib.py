@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_get_binning", "gsr_mark_visible", "gsr_depth_argsort",
     "gsr_set_timing", "gsr_stage_times", "gsr_stage_name", "gsr_set_option",
     "gsr_ply_probe", "gsr_ply_load", "gsr_disparity_colors", "gsr_pack_image",
-    "gsr_tile_row_pairs", "gsr_frame_graph_stats", "gsr_get_option", "gsr_world_bound",
+    "gsr_tile_row_pairs", "gsr_frame_graph_stats", "gsr_get_option",
 )
 
 GSR_PACK_RGBA_F32 = 0
@@ -44,7 +44,7 @@ class GsrGaussians(ctypes.Structure):
         ("means3D", ctypes.c_void_p), ("scales", ctypes.c_void_p),
         ("rotations", ctypes.c_void_p), ("opacities", ctypes.c_void_p),
         ("shs", ctypes.c_void_p), ("colors_precomp", ctypes.c_void_p),
-        ("cov3D_precomp", ctypes.c_void_p), ("bound3D", ctypes.c_void_p),
+        ("cov3D_precomp", ctypes.c_void_p),
     ]
 
 
@@ -103,7 +103,6 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.gsr_stage_name.restype = ctypes.c_char_p
     lib.gsr_set_option.argtypes = [vp, i32, i64]
     lib.gsr_get_option.argtypes = [vp, i32, ctypes.POINTER(i64)]
-    lib.gsr_world_bound.argtypes = [vp, vp, i64, vp, vp]
     lib.gsr_frame_graph_stats.argtypes = [vp, ctypes.POINTER(i64), i32]
     lib.gsr_ply_probe.argtypes = [ctypes.c_char_p, ctypes.POINTER(GsrPlyInfo)]
     lib.gsr_ply_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(GsrPlyInfo), vp, vp, vp, vp, vp,
@@ -114,7 +113,7 @@ def _declare(lib: ctypes.CDLL) -> None:
                                    ctypes.c_int32, vp, vp]
     for name in ("gsr_disparity_colors", "gsr_pack_image", "gsr_create", "gsr_reserve", "gsr_forward", "gsr_get_binning",
                  "gsr_mark_visible", "gsr_depth_argsort", "gsr_set_timing", "gsr_tile_row_pairs",
-                 "gsr_stage_times", "gsr_set_option", "gsr_get_option", "gsr_world_bound", "gsr_ply_probe", "gsr_ply_load",
+                 "gsr_stage_times", "gsr_set_option", "gsr_get_option", "gsr_ply_probe", "gsr_ply_load",
                  "gsr_frame_graph_stats"):
         getattr(lib, name).restype = i32
 

@@ -451,10 +451,6 @@ int setup_frame(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_setti
     pa.rot_vec4 = (g->rotations && (reinterpret_cast<uintptr_t>(g->rotations) & 15) == 0) ? 1 : 0;
     pa.radii = out->radii;
     pa.strip_skip = out->radii == nullptr ? 1 : 0;
-    // the per-scene bound: strip ranks without radii, covariance from scales / rotations
-    pa.bound3D = (pa.strip_skip && g->bound3D && !g->cov3D_precomp) ? g->bound3D : nullptr;
-    pa.bound_check = (pa.bound3D && f.dbg) ? static_cast<uint32_t *>(ctx->frame_words.p) + 8
-                                           : nullptr;
     pa.records = static_cast<gsr::SplatRecord *>(ctx->records.p);
     pa.sort_keys = static_cast<uint32_t *>(ctx->sort_keys.p);
     f.compact_sort = ctx->depth_sort < 0 ? (f.rows_tiles < f.gy && P >= kCompactP)
@@ -1111,19 +1107,9 @@ int forward(gsr_context *ctx, const gsr_gaussians *g, const gsr_raster_settings 
 
     if (f.tmode == 1) GSR_HIP(hipEventRecord(f.ev[0], s), "hipEventRecord");
     // ---- 1. preprocess
-    if (f.pa.bound_check)
-        GSR_HIP(hipMemsetAsync(f.pa.bound_check, 0, 8, s), "hipMemsetAsync(bound check)");
     GSR_HIP(gsr_launch_preprocess(f.pa, s), "preprocess launch");
     GSR_HIP(hipEventRecord(ctx->fork, s), "hipEventRecord(fork)");
     GSR_TRY(stage_end(ctx, f, 0));
-    if (f.pa.bound_check) {  // (debug: stage_end synchronised the stream)
-        uint32_t bc[2] = {0u, 0u};
-        GSR_HIP(hipMemcpy(bc, f.pa.bound_check, 8, hipMemcpyDeviceToHost), "hipMemcpy(bound check)");
-        if (bc[0] != 0u)
-            return fail(GSR_E_INVALID, "gsr_forward: bound3D too small: " + std::to_string(bc[0]) +
-                                           " Gaussian(s) with tiles in the strip were dropped "
-                                           "(e.g. id " + std::to_string(bc[1] - 1u) + ")");
-    }
     // MSD frames: K for the host and D for the sort from one kernel on the main stream (one
     // launch fewer than the second stream's publish plus the sort's own key-bit reduction)
     if (f.main_publish)
@@ -1430,15 +1416,6 @@ int gsr_tile_row_pairs(gsr_context *ctx, uint32_t *row_pairs, int32_t n_rows, vo
     GSR_HIP(gsr_launch_row_pairs(static_cast<const uint2 *>(ctx->ranges_local.p), ctx->last_gx,
                                  rows, row_pairs, static_cast<hipStream_t>(stream)),
             "row pairs launch");
-    return GSR_OK;
-}
-
-int gsr_world_bound(const float *scales, const float *rotations, int64_t P, float *bound,
-                    void *stream) {
-    if (P < 0 || (P > 0 && (!scales || !rotations || !bound)))
-        return fail(GSR_E_INVALID, "gsr_world_bound: bad arguments");
-    GSR_HIP(gsr_launch_world_bound(scales, rotations, P, bound, static_cast<hipStream_t>(stream)),
-            "world bound launch");
     return GSR_OK;
 }
 

@@ -255,11 +255,6 @@ struct GsrPreprocessArgs {
     uint32_t grid_x, grid_y, row_begin, row_end;
     int prefiltered;
     int sh_vec4, rot_vec4;  // 16-B aligned rows: vector loads allowed
-    // strip_skip with the per-scene bound (gsr_gaussians.bound3D, scales / rotations only): the
-    // reach test reads xyz + the bound; bound_check (debug, else NULL): device words {count, largest
-    // id + 1} of the Gaussians the bound dropped although they have a tile in the strip
-    const float *bound3D;
-    uint32_t *bound_check;
     // workspace outputs
     int32_t *radii;  // nullptr on a strip without radii: strip_skip
     int strip_skip;  // skip Gaussians whose footprint bound misses the strip (preprocess.hip)
@@ -292,9 +287,6 @@ struct GsrPreprocessArgs {
 // of the kept-key OR / AND words after them (the one definition every reader of them uses).
 inline int64_t gsr_preprocess_blocks(int64_t P) { return (P + 255) / 256; }
 hipError_t gsr_launch_preprocess(const GsrPreprocessArgs &a, hipStream_t s);
-// gsr_world_bound: the per-scene bound of each Gaussian's largest standard deviation.
-hipError_t gsr_launch_world_bound(const float *scales, const float *rotations, int64_t P,
-                                  float *bound, hipStream_t s);
 // SH -> RGB (or colors_precomp) of every Gaussian with radii > 0 into SplatRecord.c.yzw (+ rgb).
 // waves_per_simd (1..7): cap on the colour waves a CU holds at once (0 = no cap).
 hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int waves_per_simd, hipStream_t s);

@@ -253,15 +253,14 @@ __device__ __forceinline__ uint32_t col_spans(float px, float py, float A, float
     return pairs;
 }
 
-// Strip ranks without radii (strip_skip): may the Gaussian at view-space t, whose 3D covariance
-// has spectral norm at most lam3, with pixel row py have a tile in the strip?  False only when
-// provably not: from an upper bound of upstream's radius ceil(3 sqrt(lambda_max)) -- lambda_max
-// of the 2D covariance J W Sigma W^T J^T + 0.3 I is at most lam3 ||W||_F^2 ||J||_F^2 +
-// 0.3 sqrt(2), upstream's eigenvalue formula adds at most sqrt(0.1), ||J||_F^2 <= (fx^2 (1 +
-// limx^2) + fy^2 (1 + limy^2)) / z^2 (the clamped J), with 1 % and 2 px of slack for float
-// rounding -- through get_rect, which is monotone in the radius.  NaN / inf anywhere keeps the
-// Gaussian.  lam3: ||Sigma||_F of the loaded covariance, or (scale_modifier * bound3D)^2.
-__device__ __forceinline__ bool strip_reach(const GsrPreprocessArgs &a, float3 t, float lam3,
+// Strip ranks without radii (strip_skip): may the Gaussian at view-space t with 3D covariance
+// c[6] and pixel row py have a tile in the strip?  False only when provably not: from an upper
+// bound of upstream's radius ceil(3 sqrt(lambda_max)) -- lambda_max of the 2D covariance
+// J W Sigma W^T J^T + 0.3 I is at most ||Sigma||_F ||W||_F^2 ||J||_F^2 + 0.3 sqrt(2), upstream's
+// eigenvalue formula adds at most sqrt(0.1), ||J||_F^2 <= (fx^2 (1 + limx^2) + fy^2 (1 +
+// limy^2)) / z^2 (the clamped J), with 1 % and 2 px of slack for float rounding -- through
+// get_rect, which is monotone in the radius.  NaN / inf anywhere keeps the Gaussian.
+__device__ __forceinline__ bool strip_reach(const GsrPreprocessArgs &a, float3 t, const float c[6],
                                             float py) {
     const float *vm = a.viewmatrix;
     float wf = 0.0f;
@@ -272,55 +271,15 @@ __device__ __forceinline__ bool strip_reach(const GsrPreprocessArgs &a, float3 t
     const float jf = (a.focal_x * a.focal_x * (1.0f + limx * limx) +
                       a.focal_y * a.focal_y * (1.0f + limy * limy)) *
                      __builtin_amdgcn_rcpf(t.z * t.z);
-    const float lam = (lam3 * wf * jf + 0.43f) * 1.01f + 0.32f;
+    const float sf2 = c[0] * c[0] + c[3] * c[3] + c[5] * c[5] +
+                      2.0f * (c[1] * c[1] + c[2] * c[2] + c[4] * c[4]);
+    const float lam = (__builtin_sqrtf(sf2) * wf * jf + 0.43f) * 1.01f + 0.32f;
     if (!(lam < 1e30f)) return true;
     const int r = f2i_sat(__builtin_ceilf(3.0f * __builtin_sqrtf(lam) * 1.01f + 2.0f));
     const uint32_t y0 = min(a.grid_y, (uint32_t)max(0, f2i_sat((py - r) / GSR_TILE_Y)));
     const uint32_t y1 =
         min(a.grid_y, (uint32_t)max(0, f2i_sat((py + r + GSR_TILE_Y - 1) / GSR_TILE_Y)));
     return y1 > y0 && y1 > a.row_begin && y0 < a.row_end;
-}
-
-// ||Sigma||_F of a 3D covariance (upper triangle): a bound of its spectral norm.
-__device__ __forceinline__ float cov3d_frob(const float c[6]) {
-    return __builtin_sqrtf(c[0] * c[0] + c[3] * c[3] + c[5] * c[5] +
-                           2.0f * (c[1] * c[1] + c[2] * c[2] + c[4] * c[4]));
-}
-
-// The per-scene bound of gsr_world_bound: sqrt(lambda_max) of (S R)^T (S R) at modifier 1 is at
-// most ||S|| ||R(q)||, and upstream's R of a quaternion q = s q^ (not normalised) is
-// (1 - s^2) I + s^2 R(q^), so ||R|| <= |1 - s^2| + s^2; 0.1 % of margin covers the float
-// rounding of the covariance the forward builds (the reach test adds 1 % more).
-__global__ __launch_bounds__(256) void k_world_bound(const float *__restrict__ scales,
-                                                     const float *__restrict__ rot, int64_t P,
-                                                     float *__restrict__ bound) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= P) return;
-    const float sx = fabsf(scales[3 * i]), sy = fabsf(scales[3 * i + 1]),
-                sz = fabsf(scales[3 * i + 2]);
-    const float r = rot[4 * i], x = rot[4 * i + 1], y = rot[4 * i + 2], z = rot[4 * i + 3];
-    const float n2 = r * r + x * x + y * y + z * z;
-    const float b = fmaxf(fmaxf(sx, sy), sz) * (fabsf(1.0f - n2) + n2) * 1.001f + 1e-30f;
-    bound[i] = (b < 1e30f) ? b : __builtin_huge_valf();  // (NaN -> +inf: always kept)
-}
-
-// Has the Gaussian a tile in the strip (back_one's rect, nothing written)?  Debug check of a
-// bound3D rejection.
-__device__ __forceinline__ bool has_strip_tiles(const GsrPreprocessArgs &a, const float3 p_view,
-                                                float p_proj_x, float p_proj_y,
-                                                const float c[6]) {
-    const float3 cov = compute_cov2d(p_view, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy, c,
-                                     a.viewmatrix);
-    const float det = cov.x * cov.z - cov.y * cov.y;
-    if (det == 0.0f) return false;
-    const float mid = 0.5f * (cov.x + cov.z);
-    const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
-    const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
-    const int r_int = f2i_sat(ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2))));
-    const Rect rc = get_rect(ndc2pix(p_proj_x, a.W), ndc2pix(p_proj_y, a.H), r_int, a.grid_x,
-                             a.grid_y);
-    const uint32_t sy0 = max(rc.y0, a.row_begin), sy1 = min(rc.y1, a.row_end);
-    return rc.x1 > rc.x0 && sy1 > sy0;
 }
 
 // The first half of upstream preprocessCUDA for one Gaussian: every input loaded up front (so
@@ -472,42 +431,10 @@ __global__ __launch_bounds__(256) void k_preprocess(const GsrPreprocessArgs a) {
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
         bool reach = false;
         Front f;
-        if (idx < a.P && a.bound3D) {
-            // xyz + the per-scene bound decide; scale / rotation / opacity only for those that
-            // may reach the strip
-            const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1],
-                                         a.means3D[3 * idx + 2]);
-            const float beta = a.scale_modifier * a.bound3D[idx];
-            f.p_view = transform_point_4x3(p, a.viewmatrix);
-            f.in_frustum = f.p_view.z > 0.2f;
-            f.p_proj_x = f.p_proj_y = 0.0f;
-            if (f.in_frustum) {
-                const float4 p_hom = transform_point_4x4(p, a.projmatrix);
-                const float p_w = 1.0f / (p_hom.w + 0.0000001f);
-                f.p_proj_x = p_hom.x * p_w;
-                f.p_proj_y = p_hom.y * p_w;
-                reach = strip_reach(a, f.p_view, beta * beta, ndc2pix(f.p_proj_y, a.H));
-            }
-            if (reach || (a.bound_check && f.in_frustum)) {
-                const float3 s_in = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1],
-                                                a.scales[3 * idx + 2]);
-                const float4 q_in =
-                    a.rot_vec4 ? reinterpret_cast<const float4 *>(a.rotations)[idx]
-                               : make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1],
-                                             a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
-                f.opacity = a.opacities[idx];
-                compute_cov3d(s_in, a.scale_modifier, q_in, f.cov3d);
-                // debug: a Gaussian the bound dropped must have no tile in the strip
-                if (!reach && has_strip_tiles(a, f.p_view, f.p_proj_x, f.p_proj_y, f.cov3d)) {
-                    atomicAdd(a.bound_check, 1u);
-                    atomicMax(a.bound_check + 1, (uint32_t)idx + 1u);
-                }
-            }
-            if (!reach) none_one(a, idx);
-        } else if (idx < a.P) {
+        if (idx < a.P) {
             f = front_one(a, idx);
             reach = f.in_frustum &&
-                    strip_reach(a, f.p_view, cov3d_frob(f.cov3d), ndc2pix(f.p_proj_y, a.H));
+                    strip_reach(a, f.p_view, f.cov3d, ndc2pix(f.p_proj_y, a.H));
             if (!reach) none_one(a, idx);
         }
         const uint64_t bal = __ballot(reach);
@@ -815,14 +742,6 @@ hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int waves_per_simd, hipS
 hipError_t gsr_color_setup() {
     return hipFuncSetAttribute(reinterpret_cast<const void *>(&k_color),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-}
-
-hipError_t gsr_launch_world_bound(const float *scales, const float *rotations, int64_t P,
-                                  float *bound, hipStream_t s) {
-    if (P == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_world_bound, dim3(grid_for(P)), dim3(256), 0, s, scales, rotations, P,
-                       bound);
-    return hipGetLastError();
 }
 
 bool gsr_color_ids_ok(const GsrPreprocessArgs &a) {

@@ -69,7 +69,7 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
                                scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tanfovx,
                                tanfovy, image_height, image_width, sh, degree, campos, prefiltered,
                                debug, *, tile_rows=None, extras=(), stream=None, slot=0,
-                               out_color=None, radii=True, bound3D=None) -> ForwardResult:
+                               out_color=None, radii=True) -> ForwardResult:
     """Same arguments, order and validation as upstream `_C.rasterize_gaussians`.
 
     Extensions (keyword-only, for the strip partition and the parity tests):
@@ -103,10 +103,6 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
     viewmatrix = _as_dev(viewmatrix, device, "4,4")
     projmatrix = _as_dev(projmatrix, device, "4,4")
     campos = _as_dev(campos, device, "3")
-    if bound3D is not None:
-        bound3D = _as_dev(bound3D, device, "P")
-        if bound3D.numel() != P:
-            raise RuntimeError("bound3D must have P entries")
 
     M = 0
     if sh is not None:
@@ -156,7 +152,7 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
                           means3D=_lib.ptr(means3D), scales=_lib.ptr(scales),
                           rotations=_lib.ptr(rotations), opacities=_lib.ptr(opacities),
                           shs=_lib.ptr(sh), colors_precomp=_lib.ptr(colors_precomp),
-                          cov3D_precomp=_lib.ptr(cov3D_precomp), bound3D=_lib.ptr(bound3D))
+                          cov3D_precomp=_lib.ptr(cov3D_precomp))
     st = _lib.GsrRasterSettings(image_width=W, image_height=H, tanfovx=float(tanfovx),
                                 tanfovy=float(tanfovy), viewmatrix=_lib.ptr(viewmatrix),
                                 projmatrix=_lib.ptr(projmatrix), campos=_lib.ptr(campos),
@@ -174,26 +170,6 @@ def rasterize_gaussians_native(bg, means3D, colors_precomp, opacities, scales, r
         _lib.check(lib.gsr_forward(ctx, ctypes.byref(g), ctypes.byref(st), ctypes.byref(out),
                                    ctypes.c_void_p(stream)), "gsr_forward")
     return ForwardResult(int(out.num_rendered), color, radii, ext)
-
-
-def world_bound(scales: torch.Tensor, rotations: torch.Tensor, stream=None) -> torch.Tensor:
-    """Per-scene bound of every Gaussian's largest standard deviation (gsr_world_bound), for
-    strip forwards (rasterize_gaussians_native(..., radii=False, bound3D=...)).  It depends only on
-    the scales and rotations, so the viewer computes it once when the scene is loaded
-    (HIPRenderer.update_gaussian_data, the hook of renderer_cuda.py:135-137)."""
-    device = _device_of(scales)
-    P = int(scales.size(0))
-    scales = _as_dev(scales, device, "P,3")
-    rotations = _as_dev(rotations, device, "P,4")
-    out = torch.empty((P,), dtype=torch.float32, device=device)
-    if stream is None:
-        stream = torch.cuda.current_stream(device).cuda_stream
-    dev_index = device.index if device.index is not None else torch.cuda.current_device()
-    with torch.cuda.device(dev_index):
-        _lib.check(_lib.load_library().gsr_world_bound(
-            _lib.ptr(scales), _lib.ptr(rotations), P, _lib.ptr(out), ctypes.c_void_p(stream)),
-            "gsr_world_bound")
-    return out
 
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,

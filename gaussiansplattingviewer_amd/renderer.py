@@ -19,8 +19,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .rasterizer import (GaussianRasterizationSettings, GaussianRasterizer,
-                         rasterize_gaussians_native, world_bound)
+from .rasterizer import GaussianRasterizationSettings, GaussianRasterizer, rasterize_gaussians_native
 
 
 class GaussianRenderBase:
@@ -62,9 +61,6 @@ class GaussianDataHIP:
     scale: torch.Tensor
     opacity: torch.Tensor
     sh: torch.Tensor
-    # per-scene bound of each Gaussian's largest standard deviation (rasterizer.world_bound),
-    # computed at load for strip forwards; None until update_gaussian_data
-    bound3D: torch.Tensor | None = None
 
     def __len__(self):
         return len(self.xyz)
@@ -118,9 +114,6 @@ class HIPRenderer(GaussianRenderBase):
         the device (e.g. ply.load_ply(path, device=...)) is used as is."""
         self.gaussians = gaus if isinstance(gaus, GaussianDataHIP) else gaus_hip_from_cpu(gaus, self.device)
         self.raster_settings["sh_degree"] = int(np.round(np.sqrt(self.gaussians.sh_dim))) - 1
-        # the load-time hook: the camera-independent bound a strip forward reaches with
-        if self.gaussians.bound3D is None and len(self.gaussians):
-            self.gaussians.bound3D = world_bound(self.gaussians.scale, self.gaussians.rot)
 
     def sort_and_update(self, camera, use_file=False, pose=None):
         pass  # the rasterizer sorts on the device every frame
@@ -202,7 +195,7 @@ class HIPRenderer(GaussianRenderBase):
                     rs.bg, g.xyz, colors, g.opacity, g.scale, g.rot, rs.scale_modifier, None,
                     rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height,
                     rs.image_width, shs, rs.sh_degree, rs.campos, rs.prefiltered, rs.debug,
-                    tile_rows=self.tile_rows, bound3D=g.bound3D)
+                    tile_rows=self.tile_rows)
                 img, radii = res.color, res.radii
         self.image, self.radii = img, radii
         return img

@@ -49,8 +49,7 @@ extern "C" {
 /* 2 (round 4): option ids renumbered (GSR_OPT_COLUMN_PAIRS retired, tight binning moved to 13,
  * ids 10 and 12 reserved), GSR_OPT_DEPTH_SORT (id 11, was COMPACT_SORT) gains the MSD form,
  * gsr_get_binning exports tight lists.
- * 3 (round 6): gsr_get_option; contexts are serialised by a mutex and ordered across streams;
- * gsr_gaussians.bound3D and gsr_world_bound (the strip ranks' load-time bound). */
+ * 3 (round 6): gsr_get_option; contexts are serialised by a mutex and ordered across streams. */
 #define GSR_ABI_VERSION 3
 
 enum {
@@ -78,14 +77,6 @@ typedef struct {
     const float *shs;            /* [P,M,3] */
     const float *colors_precomp; /* [P,3]  */
     const float *cov3D_precomp;  /* [P,6]  upper triangle xx,xy,xz,yy,yz,zz */
-    /* optional [P] (ABI 3): gsr_world_bound's per-scene bound of each Gaussian's largest
-     * standard deviation, computed once when the scene is loaded (the viewer's load-time hook:
-     * update_gaussian_data -> gaus_cuda_from_cpu, renderer_cuda.py:87-98, 135-137).  A strip
-     * forward without radii then decides from xyz + this word (16 B) whether the Gaussian can
-     * reach the strip, and reads its scale / rotation / opacity only if so.  Ignored with
-     * cov3D_precomp or on whole frames; NULL keeps the bound from the loaded covariance.  A
-     * bound smaller than gsr_world_bound's is caught in debug mode (GSR_E_INVALID). */
-    const float *bound3D;
 } gsr_gaussians;
 
 /* GaussianRasterizationSettings (renderer_cuda.py:104-117). */
@@ -158,14 +149,6 @@ int gsr_get_binning(gsr_context *ctx, uint32_t *point_list, uint32_t *point_tile
  * next boundaries by these counts.  No reference counterpart: the reference renders each frame
  * on one device (renderer_cuda.py:205-224). */
 int gsr_tile_row_pairs(gsr_context *ctx, uint32_t *row_pairs, int32_t n_rows, void *stream);
-
-/* Per-scene world-space bound (ABI 3), for gsr_gaussians.bound3D: bound[i] >= sqrt(lambda_max)
- * of Gaussian i's 3D covariance (S R)^T (S R) at scale_modifier 1, as upstream computeCov3D
- * builds it from scales[i] and the (not normalised) quaternion rotations[i]:
- * max|s| (|1 - |q|^2| + |q|^2) with a rounding margin; +inf for non-finite inputs.  A forward
- * scales it by its scale_modifier.  Depends only on the scene, not on the camera. */
-int gsr_world_bound(const float *scales, const float *rotations, int64_t P, float *bound,
-                    void *stream);
 
 /* GaussianRasterizer.markVisible: visible[i] = view-space z > 0.2. */
 int gsr_mark_visible(gsr_context *ctx, const float *means3D, int64_t P, const float *viewmatrix,

@@ -8,8 +8,7 @@ import contextlib
 
 from gaussiansplattingviewer_amd import _lib
 from gaussiansplattingviewer_amd.camera import cuda_camera_inputs
-from gaussiansplattingviewer_amd.rasterizer import (binning_state, rasterize_gaussians_native,
-                                                    world_bound)
+from gaussiansplattingviewer_amd.rasterizer import binning_state, rasterize_gaussians_native
 
 ALL_EXTRAS = ("depths", "means2D", "conic_opacity", "rgb", "tiles_touched", "final_T", "n_contrib")
 
@@ -53,14 +52,9 @@ def to_dev(a, dev):
 
 
 def run_hip(s, dev, tile_rows=None, colors_precomp=None, cov3D_precomp=None, extras=ALL_EXTRAS,
-            binning=True, debug=False, radii=True, bound=None):
-    """bound: None, "world" (gsr_world_bound of the scene) or an array of P floats (bound3D)."""
+            binning=True, debug=False, radii=True):
     g = s["g"]
     P = len(g.xyz)
-    if isinstance(bound, str):
-        bound = world_bound(to_dev(g.scale, dev), to_dev(g.rot, dev))
-    elif bound is not None:
-        bound = to_dev(np.asarray(bound, np.float32), dev)
     sh = None if colors_precomp is not None else to_dev(g.sh.reshape(P, g.sh.shape[-1] // 3, 3), dev)
     use_sr = cov3D_precomp is None
     res = rasterize_gaussians_native(
@@ -69,7 +63,7 @@ def run_hip(s, dev, tile_rows=None, colors_precomp=None, cov3D_precomp=None, ext
         to_dev(g.rot, dev) if use_sr else None, s["scale_modifier"], to_dev(cov3D_precomp, dev),
         to_dev(s["view"], dev), to_dev(s["proj"], dev), s["tx"], s["ty"], s["H"], s["W"], sh,
         s["sh_degree"], to_dev(s["campos"], dev), False, debug, tile_rows=tile_rows,
-        extras=extras, radii=radii, bound3D=bound)
+        extras=extras, radii=radii)
     out = {"num_rendered": res.num_rendered, "color": res.color.cpu().numpy(),
            "radii": None if res.radii is None else res.radii.cpu().numpy()}
     for k, v in res.extras.items():

@@ -134,9 +134,8 @@ def test_c4_strips_equal_full_frame_rows(gpu, c4, c4_hip, rank):
                                   full["ranges"][t0:t1][nonempty] - lo)
 
 
-@pytest.mark.parametrize("rank,bound", [(0, None), (3, None), (7, None), (0, "world"),
-                                        (3, "world"), (7, "world")])
-def test_c4_strips_without_radii(gpu, c4, c4_hip, rank, bound):
+@pytest.mark.parametrize("rank", [0, 3, 7])
+def test_c4_strips_without_radii(gpu, c4, c4_hip, rank):
     """A strip rank without the radii output (gsr_outputs.radii NULL, the multi-GPU bench's
     call) skips the Gaussians whose footprint bound misses its strip -- here with the C4 strips'
     compaction and colour-id path: image and binning stay bit-identical to the full frame."""
@@ -145,8 +144,7 @@ def test_c4_strips_without_radii(gpu, c4, c4_hip, rank, bound):
     W, H = s["W"], s["H"]
     gx, gy = (W + 15) // 16, (H + 15) // 16
     rows = strip_rows(gy, 8, rank)
-    part = run_hip(s, gpu, tile_rows=rows, extras=("final_T", "n_contrib"), radii=False,
-                   bound=bound)
+    part = run_hip(s, gpu, tile_rows=rows, extras=("final_T", "n_contrib"), radii=False)
     assert part["radii"] is None
     y0, n = strip_pixel_rows(rows, H)
     np.testing.assert_array_equal(part["color"].view(np.uint32),

@@ -16,8 +16,7 @@ from gaussiansplattingviewer_amd.camera import Camera, static_camera
 from gaussiansplattingviewer_amd.gaussian_data import (GaussianData, naive_gaussian,
                                                        synthetic_gaussians)
 
-from gpu_helpers import (assert_image_close, assert_parity, run_hip, run_oracle, scene_inputs,
-                         to_dev)
+from gpu_helpers import (assert_image_close, assert_parity, run_hip, run_oracle, scene_inputs)
 
 pytestmark = pytest.mark.gpu
 
@@ -210,71 +209,11 @@ def test_strips_equal_full_frame_rows(gpu, world):
         np.testing.assert_array_equal(part["point_list"], full["point_list"][sel])
         np.testing.assert_array_equal(part["point_tiles"], full["point_tiles"][sel])
         K_sum += part["num_rendered"]
-        # without radii (a strip rank's call): Gaussians that miss the strip are skipped, by the
-        # loaded covariance or by the per-scene world-space bound (bound3D)
-        for bound in (None, "world"):
-            lean = run_hip(s, gpu, tile_rows=rows, extras=("final_T", "n_contrib"), radii=False,
-                           bound=bound)
-            for k in ("color", "n_contrib", "final_T", "point_list", "ranges"):
-                np.testing.assert_array_equal(lean[k], part[k], err_msg=f"{k} bound={bound}")
+        # without radii (a strip rank's call): Gaussians that miss the strip are skipped
+        lean = run_hip(s, gpu, tile_rows=rows, extras=("final_T", "n_contrib"), radii=False)
+        for k in ("color", "n_contrib", "final_T", "point_list", "ranges"):
+            np.testing.assert_array_equal(lean[k], part[k], err_msg=k)
     assert K_sum == full["num_rendered"]
-
-
-def test_world_bound_bounds_the_covariance(gpu):
-    """gsr_world_bound >= sqrt(lambda_max) of upstream's covariance (S R(q))^T (S R(q)) for
-    activated and raw scales and normalised, unnormalised and degenerate quaternions (float64
-    eigenvalues of the float32 inputs), +inf for non-finite inputs."""
-    import torch
-    from gaussiansplattingviewer_amd.rasterizer import world_bound
-    rng = np.random.default_rng(31)
-    n = 50_000
-    s = np.exp(rng.normal(-3.0, 1.5, (n, 3))).astype(np.float32)
-    s[: n // 10] *= -1.0  # (raw, negative scales: |s| bounds them)
-    q = rng.normal(0.0, 1.0, (n, 4)).astype(np.float32)
-    q[n // 2:] *= rng.uniform(0.0, 3.0, (n - n // 2, 1)).astype(np.float32)  # |q| != 1
-    q[n // 3: n // 3 + 10] = 0.0
-    s[7] = np.nan
-    q[8, 2] = np.inf
-    b = world_bound(torch.as_tensor(s).to(gpu), torch.as_tensor(q).to(gpu)).cpu().numpy()
-    assert np.isinf(b[7]) and np.isinf(b[8])
-    ok = np.ones(n, bool)
-    ok[[7, 8]] = False
-    s64, q64 = s[ok].astype(np.float64), q[ok].astype(np.float64)
-    r, x, y, z = q64.T
-    R = np.stack([np.stack([1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y)], -1),
-                  np.stack([2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x)], -1),
-                  np.stack([2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)], -1)],
-                 -2)
-    M = s64[:, :, None] * R
-    lam = np.linalg.eigvalsh(np.einsum("nji,njk->nik", M, M))[:, -1]
-    assert np.all(b[ok].astype(np.float64) >= np.sqrt(np.maximum(lam, 0.0)))
-    # and not loose by much for normalised quaternions (|1 - |q|^2| + |q|^2 = 1)
-    unit = np.abs(np.linalg.norm(q64, axis=1) - 1.0) < 1e-3
-    assert unit.sum() == 0 or np.all(b[ok][unit] <= 1.01 * np.abs(s64[unit]).max(axis=1) + 1e-6)
-
-
-def test_too_small_bound_is_caught_in_debug_mode(gpu):
-    """A bound3D smaller than the covariance's (here half of gsr_world_bound's) drops
-    Gaussians that reach the strip: debug mode reports it (GSR_E_INVALID), and with the true
-    bound the debug forward passes and equals the full frame's rows."""
-    import torch
-    from gaussiansplattingviewer_amd.rasterizer import world_bound
-    from gaussiansplattingviewer_amd.strips import strip_pixel_rows, strip_rows
-    W, H = 960, 540
-    s = scene_inputs(synthetic_gaussians(60_000, 3, 33), static_camera(W, H), 3,
-                     scale_modifier=1.3)
-    g = s["g"]
-    wb = world_bound(to_dev(g.scale, gpu), to_dev(g.rot, gpu)).cpu().numpy()
-    rows = strip_rows((H + 15) // 16, 4, 1)
-    full = run_hip(s, gpu, binning=False)
-    ok = run_hip(s, gpu, tile_rows=rows, extras=(), radii=False, debug=True, bound=wb,
-                 binning=False)
-    y0, n = strip_pixel_rows(rows, H)
-    np.testing.assert_array_equal(ok["color"].view(np.uint32),
-                                  full["color"][:, y0:y0 + n].view(np.uint32))
-    with pytest.raises(RuntimeError, match="bound3D too small"):
-        run_hip(s, gpu, tile_rows=rows, extras=(), radii=False, debug=True, bound=wb * 0.25,
-                binning=False)
 
 
 def test_cost_weighted_strips_on_a_crowded_scene(gpu):
