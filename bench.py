@@ -80,8 +80,9 @@ def parse():
                          "operation order")
     ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight (FramePipeline: own stream + context slot each); "
-                         "1 = serial forwards (default: 4 full frames, each on one stream; 2 "
-                         "strip frames, each with its second stream and frame graphs)")
+                         "1 = serial forwards (default: 4 frames, each on one stream -- strip "
+                         "frames below 4M Gaussians with the deferred-K chains; 2 larger strip "
+                         "frames, each with its second stream and frame graphs)")
     ap.add_argument("--depth-sort", default="auto", choices=["auto", "lsd", "compact", "msd", "compact-msd"],
                     help="GSR_OPT_DEPTH_SORT: LSD passes, LSD after compacting the kept keys, or "
                          "the MSD pass + per-bucket local sort (auto: compact on strips of >= 4M "
@@ -362,10 +363,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.inflight is None:
-        # full frames: four in flight, each on one stream (DESIGN.md decision 13); strip frames
-        # (a rank of an N-GPU frame): two, with second streams and frame graphs (decision 12)
-        args.inflight = 2 if (world > 1 or args.sim_strip) else 4
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         if world == 1:
             raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
@@ -376,6 +373,17 @@ def main():
                                 device_id=torch.device("cuda", local))
 
     scene = Scene(args.config, dev)
+    # Frames in flight.  Full frames: four, each on one stream (DESIGN.md decision 13).  Strip
+    # frames (a rank of an N-GPU frame, or the simulated strip) of scenes below the compacting
+    # sort's 4M Gaussians (the headline's 1M): four one-stream frames too, with the deferred-K
+    # chains (GSR_OPT_FRAME_GRAPHS 2: the host does not wait for K in mid-frame) -- C3 strips
+    # 10,300-10,450 -> 12,100-12,350 frames/s; larger strips (C4's 6M): two frames with their
+    # second streams replaying frame graphs (decision 12), 4 % faster there than four one-stream
+    # frames (profiles/r06g_ab_strip_depth.txt)
+    strip = world > 1 or bool(args.sim_strip)
+    small_strip = strip and scene.P < (4 << 20)
+    if args.inflight is None:
+        args.inflight = 2 if (strip and not small_strip) else 4
     W, H = scene.W, scene.H
     gy, gx = (H + 15) // 16, (W + 15) // 16
     rows = None
@@ -394,11 +402,11 @@ def main():
               if world > 1 else None)
     balancer = StripBalancer(gy, gx, world, rank, device=dev) if world > 1 else None
     # frames in flight: frame i renders on stream i % D with context slot i % D, so the next
-    # frame's latency-bound preprocess / sort / binning overlap this frame's blend
-    # strip frames (a rank of an N-GPU frame, or the simulated strip) replay frame graphs: with
-    # two in flight a strip rank's rate is then steady instead of bimodal run to run (DESIGN.md
-    # decision 12); full frames keep direct launches
-    strip_graphs = args.inflight >= 2 and (world > 1 or bool(args.sim_strip))
+    # frame's latency-bound preprocess / sort / binning overlap this frame's blend.  Large strip
+    # frames in pairs replay frame graphs (mode 1: with two in flight a strip rank's rate is then
+    # steady instead of bimodal run to run, DESIGN.md decision 12); small strip frames launch the
+    # deferred-K chains directly on one stream each (mode 2); full frames keep direct launches
+    strip_graphs = args.inflight >= 2 and strip and not small_strip
     pipe = None  # (created below: after the serial passes on one GPU)
     if world > 1:
         # RCCL's communicators (and their streams) first: one all-reduce and one gather of an
@@ -446,7 +454,8 @@ def main():
             {"auto": -1, "lsd": 0, "compact": 1, "msd": 2, "compact-msd": 3}[args.depth_sort])
     # frame graphs: the pipeline's choice (strip frames in flight) unless --graphs; the serial
     # passes render as a caller without the pipeline does (direct launches)
-    graphs_inflight = args.graphs if args.graphs is not None else int(strip_graphs)
+    graphs_inflight = (args.graphs if args.graphs is not None else
+                       1 if strip_graphs else 2 if small_strip else 0)
     graphs_serial = args.graphs if args.graphs is not None else 0
     names = _lib.stage_names()
     buf = (ctypes.c_float * len(names))()
@@ -493,9 +502,8 @@ def main():
                          second_stream=None if args.second_stream is None
                          else bool(args.second_stream))
     for c in ctxs:
-        if args.graphs is not None:
-            _lib.check(lib.gsr_set_option(c, _lib.GSR_OPT_FRAME_GRAPHS, args.graphs),
-                       "gsr_set_option")
+        _lib.check(lib.gsr_set_option(c, _lib.GSR_OPT_FRAME_GRAPHS, graphs_inflight),
+                   "gsr_set_option")
 
     # (1) The blend's event time with frames in flight (events around the blend on every 8th
     # forward of slot 0; these frames run on the stream path).
@@ -653,9 +661,11 @@ def main():
         "frame_graphs": {"timed_frames": graphs_inflight, "serial_pass": graphs_serial,
                          **{f"slot{c}": _lib.frame_graph_stats(local, c)
                             for c in range(args.inflight)},
-                         "note": "GSR_OPT_FRAME_GRAPHS of the in-flight frames (recorded graphs "
-                                 "for strip frames, direct launches for full frames) and of the "
-                                 "serial pass (direct launches, as a caller without the pipeline)"},
+                         "note": "GSR_OPT_FRAME_GRAPHS of the in-flight frames (0 direct "
+                                 "launches: full frames; 2 deferred-K chains on one stream: "
+                                 "strip frames below 4M Gaussians; 1 recorded graphs: larger "
+                                 "strip frames, two in flight) and of the serial pass (direct "
+                                 "launches, as a caller without the pipeline)"},
         "serial_ms_per_frame": round(serial_ms, 4),
         "serial_note": "one frame in flight at a time (no FramePipeline overlap), this rank",
         "roofline": roofline,
