@@ -814,16 +814,14 @@ void finish_frame(gsr_context *ctx, const Frame &f, gsr_outputs *out) {
 // num_rendered) and re-renders an overflowed frame the direct way with a larger capacity, so
 // every returned image is complete.
 
-// Eligible forwards: the second stream on (the second chain is recorded and replayed there),
-// column-first binning, a known capacity, no debug, no per-stage timing, no
+// Eligible forwards: column-first binning, a known capacity, no debug, no per-stage timing, no
 // compaction (its colour pass waits on a mid-chain event of the frame stream), no rgb output
 // (the colour pass's).
-// (Mode 2 also runs one-stream frames: the second stream's chain then runs in order on the
-// frame's stream, as the direct path's one-stream frames do.)
+// (One-stream frames too: the second stream's chain then runs in order on the frame's stream,
+// as the direct path's one-stream frames do -- recorded as its own graph in mode 1.)
 bool graph_eligible(const gsr_context *ctx, const Frame &f, const gsr_outputs *out) {
-    return ctx->graphs && (ctx->second_stream || ctx->graphs == 2) && ctx->list_cap > 0 &&
-           f.colpairs && !f.dbg && f.tmode != 1 && !f.compact_sort && !f.color_ids && !out->rgb &&
-           f.P > 0;
+    return ctx->graphs && ctx->list_cap > 0 && f.colpairs && !f.dbg && f.tmode != 1 &&
+           !f.compact_sort && !f.color_ids && !out->rgb && f.P > 0;
 }
 
 GraphKey graph_key(const gsr_context *ctx, const Frame &f) {
@@ -892,9 +890,27 @@ int drain_retired(gsr_context *ctx, hipStream_t s, bool force) {
 // GPU_MAX_HW_QUEUES = 4 hardware queues, which the frame streams and second streams of two frames
 // in flight already fill: with it, every stream shares a queue and the direct path lost 20 % in
 // flight).
+// A context without its second stream (one-stream frames) captures on a stream made for the
+// recording and destroyed right after it: it holds no hardware queue beyond the recording, which
+// happens once per key.
+struct CaptureStream {
+    hipStream_t s = nullptr;
+    bool own = false;
+    ~CaptureStream() {
+        if (own && s) (void)hipStreamDestroy(s);
+    }
+};
+
 template <typename Chain>
 int record_chain(gsr_context *ctx, Chain chain, hipGraphExec_t *out) {
-    hipStream_t cs = ctx->aux;
+    CaptureStream capture;
+    capture.s = ctx->aux;
+    if (!capture.s) {
+        GSR_HIP(hipStreamCreateWithFlags(&capture.s, hipStreamNonBlocking),
+                "hipStreamCreateWithFlags(capture)");
+        capture.own = true;
+    }
+    hipStream_t cs = capture.s;
     GSR_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
     const int rc = chain(cs);
     hipGraph_t graph = nullptr;
@@ -1025,7 +1041,7 @@ int forward_graph(gsr_context *ctx, Frame &f, const gsr_raster_settings *st, gsr
     else GSR_TRY(chain_sort(ctx, g, s));
     const bool two = ctx->second_stream != 0;  // (else mode 2 on one stream: in order on s)
     if (two) GSR_HIP(hipStreamWaitEvent(ctx->aux, ctx->fork, 0), "hipStreamWaitEvent(fork)");
-    if (replay) GSR_HIP(hipGraphLaunch(e->aux, ctx->aux), "hipGraphLaunch(second stream)");
+    if (replay) GSR_HIP(hipGraphLaunch(e->aux, two ? ctx->aux : s), "hipGraphLaunch(aux chain)");
     else GSR_TRY(aux_chain(ctx, g, two ? ctx->aux : s, fw));
     if (two) GSR_HIP(hipEventRecord(ctx->join, ctx->aux), "hipEventRecord(join)");
     uint32_t *point_list = nullptr;

@@ -253,8 +253,9 @@ const char *gsr_stage_name(int i);
  *     binning.  0: they run in order on the frame's own stream and the second stream is
  *     destroyed, so the context holds one hardware queue instead of two -- with the process's
  *     GPU_MAX_HW_QUEUES = 4, four frames in flight on four contexts then each have a queue of
- *     their own (FramePipeline with depth >= 3; DESIGN.md decision 13).  Frame graphs need the
- *     second stream and are not used while it is 0.  The image is the same either way.
+ *     their own (FramePipeline with depth >= 3; DESIGN.md decision 13).  With 0, frame graphs
+ *     (GSR_OPT_FRAME_GRAPHS) run the second stream's chain in order on the frame's stream (mode
+ *     1 records it on a stream made for the recording; ABI 3).  The image is the same either way.
  * The binning form is chosen per frame: column-first (the first tile-sort pass on (Gaussian,
  * tile column) segments, the second on packed (tile row, Gaussian id) words) up to 256 tile
  * columns and strip rows, else the per-pair form; both produce the same lists.  Ids 10 and 12

@@ -23,13 +23,13 @@ _next_slot = [20]
 
 def _slots(dev, mode=1):
     """A fresh (graphs on, graphs off) pair of context slots; mode 1 replays recorded graphs, 2
-    launches the same deferred-K chains directly, "2-one-stream" does that on a context without
-    its second stream (the second stream's chain in order on the frame's stream, as four frames
-    in flight run)."""
+    launches the same deferred-K chains directly; "1-one-stream" / "2-one-stream" do that on a
+    context without its second stream (the second stream's chain in order on the frame's stream,
+    as four frames in flight run; mode 1 records it on a stream made for the recording)."""
     on, off = _next_slot[0], _next_slot[0] + 1
     _next_slot[0] += 2
-    one = mode == "2-one-stream"
-    set_option(dev, _lib.GSR_OPT_FRAME_GRAPHS, 2 if one else mode, on)
+    one = isinstance(mode, str)
+    set_option(dev, _lib.GSR_OPT_FRAME_GRAPHS, int(mode[0]) if one else mode, on)
     set_option(dev, _lib.GSR_OPT_FRAME_GRAPHS, 0, off)
     set_option(dev, _lib.GSR_OPT_SECOND_STREAM, 0 if one else 1, on)
     set_option(dev, _lib.GSR_OPT_SECOND_STREAM, 0 if one else 1, off)
@@ -80,7 +80,7 @@ CASES = {
 }
 
 
-@pytest.mark.parametrize("mode", [1, 2, "2-one-stream"])
+@pytest.mark.parametrize("mode", [1, 2, "1-one-stream", "2-one-stream"])
 @pytest.mark.parametrize("case", sorted(CASES))
 def test_graph_frames_equal_direct(gpu, case, mode):
     build, W, H, tile_rows, radii = CASES[case]
@@ -115,7 +115,7 @@ def test_graph_frames_precomputed_colours(gpu):
     assert _lib.frame_graph_stats(0, on)["graph_frames"] >= 3
 
 
-@pytest.mark.parametrize("mode", [1, 2, "2-one-stream"])
+@pytest.mark.parametrize("mode", [1, 2, "1-one-stream", "2-one-stream"])
 def test_graph_overflow_rerenders(gpu, mode):
     """A small scene sets the capacity; a much larger one on the same context overflows it on
     its first frame (rendered again the direct way, identical), then runs on graphs again."""

@@ -72,6 +72,7 @@ def _worker(rank, world, port, out_path, depth):
         for slot in range(depth):
             _lib.set_option(_lib.context(0, slot), _lib.GSR_OPT_FRAME_GRAPHS, 0)
         pipe.close()
+        if rank == 0:
             ok = [bool(torch.equal(fr.view(torch.int32), full.view(torch.int32))) for fr in frames]
             np.save(out_path, np.array(ok + [len(bal.history)], dtype=np.int64))
     finally:
