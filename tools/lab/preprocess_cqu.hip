@@ -779,10 +779,8 @@ hipError_t gsr_launch_color(const GsrPreprocessArgs &a, int waves_per_simd, hipS
     // a 4-wave block puts one wave on each SIMD: w blocks per CU = w waves per SIMD, held by
     // reserving 1/w of the CU's 160 KiB of LDS per block (1 KiB granules; the kernel's dynamic
     // LDS limit is raised once per device, gsr_color_setup)
-    size_t lds = (waves_per_simd >= 1 && waves_per_simd < 8)
-                     ? (size_t)(160 * 1024 / waves_per_simd) & ~(size_t)1023
-                     : 0;
-    if (lds < kColorLds) lds = kColorLds;  // (the staged rows)
+    (void)waves_per_simd;  // lab: uncapped (whole lines per load: no L1 thrash to cap)
+    const size_t lds = kColorLds;
     hipLaunchKernelGGL(k_color, dim3(g0), dim3(256), lds, s, a);
     return hipGetLastError();
 }
