@@ -453,8 +453,9 @@ __global__ __launch_bounds__(kCG) void k_col_count(const uint32_t *__restrict__ 
     __shared__ uint32_t s_diff[kCGroup][kRadixBins + 1];
     __shared__ uint32_t s_tmp[4];
     const int tid = threadIdx.x;
+    const uint32_t gb = xcd_run_block(blockIdx.x, gridDim.x, kXcdColChunk);  // the group
     const int64_t n = *d_n;
-    const int64_t base = (int64_t)blockIdx.x * (kCG * kCGroup);
+    const int64_t base = (int64_t)gb * (kCG * kCGroup);
     if (base >= n) return;  // whole group (k_rs_scan reads groups [0, ceil(n / 1024)) only)
     for (int i = tid; i < kCGroup * (kRadixBins + 1); i += kCG) (&s_diff[0][0])[i] = 0u;
     uint2 r[kCGroup], q[kCGroup];
@@ -495,7 +496,7 @@ __global__ __launch_bounds__(kCG) void k_col_count(const uint32_t *__restrict__ 
     }
     __syncthreads();
     uint32_t run = 0;
-    uint32_t *o = off + (int64_t)blockIdx.x * kCGroup * kRadixBins;
+    uint32_t *o = off + (int64_t)gb * kCGroup * kRadixBins;
 #pragma unroll
     for (int j = 0; j < kCGroup; ++j) {
         uint32_t tot;
@@ -504,7 +505,7 @@ __global__ __launch_bounds__(kCG) void k_col_count(const uint32_t *__restrict__ 
         o[j * kRadixBins + tid] = run;
         run += c;
     }
-    hist[(int64_t)tid * ng + blockIdx.x] = run;
+    hist[(int64_t)tid * ng + gb] = run;
 }
 
 __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict__ perm,
@@ -522,14 +523,15 @@ __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict_
         RadixTileSmem<kCW, kCIt / 2> small;
     } sm;
     const int tid = threadIdx.x;
+    const uint32_t blk = xcd_run_block(blockIdx.x, gridDim.x, kXcdColChunk);
     // global start of column d for this block's segments: all earlier columns (then earlier
     // blocks, below); the total is the list length
     uint32_t tot;
     const uint32_t dstart = block256_exclusive_scan(digit_total[tid], c.tmp, tot);
-    if (list_n && blockIdx.x == 0 && tid == 0) *list_n = tot;  // (frame graphs: the row pass)
+    if (list_n && blk == 0 && tid == 0) *list_n = tot;  // (frame graphs: the row pass)
     if (tot > cap) return;  // (frame graphs) the list does not fit: the host re-renders
     const int64_t n = *d_n;
-    const int64_t base = (int64_t)blockIdx.x * kCG;
+    const int64_t base = (int64_t)blk * kCG;
     if (base >= n) return;
     const int64_t e = base + tid;
     const bool valid = e < n;
@@ -546,8 +548,8 @@ __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict_
     c.cols_lo[tid] = q.x;
     c.cols_hi[tid] = q.y;
     c.id[tid] = valid ? perm[e] : 0u;
-    c.colbase[tid] = dstart + hist[(int64_t)tid * ng + blockIdx.x / kCGroup] +
-                     off[(int64_t)blockIdx.x * kRadixBins + tid];
+    c.colbase[tid] = dstart + hist[(int64_t)tid * ng + blk / kCGroup] +
+                     off[(int64_t)blk * kRadixBins + tid];
     // thread t owns segments [seg0, seg0 + w) (one per column of its rect)
     uint32_t nseg;
     const uint32_t seg0 = block256_exclusive_scan(r.x >> 16, c.tmp, nseg);
@@ -930,8 +932,9 @@ hipError_t gsr_launch_col_pairs_count(const uint32_t *perm, const uint2 *strip_r
     const int64_t nb = (n_max + kCG - 1) / kCG, ng = (nb + kCGroup - 1) / kCGroup;
     if (nb == 0) return hipSuccess;
     uint32_t *off = hist + ng * kRadixBins;
-    hipLaunchKernelGGL(k_col_count, dim3((unsigned)ng), dim3(kCG), 0, s, perm, strip_rect,
-                       strip_rc, d_n, rect_sorted, rc_sorted, hist, ng, off);
+    const dim3 grid(xcd_run_grid(ng, kXcdColChunk));
+    hipLaunchKernelGGL(k_col_count, grid, dim3(kCG), 0, s, perm, strip_rect, strip_rc, d_n,
+                       rect_sorted, rc_sorted, hist, ng, off);
     return gsr_launch_digit_scan_n(hist, ng, digit_total, d_n, kCG * kCGroup, s);
 }
 
@@ -943,7 +946,8 @@ hipError_t gsr_launch_col_pairs_scatter(const uint32_t *perm, const uint2 *rect_
     const int64_t nb = (n_max + kCG - 1) / kCG, ng = (nb + kCGroup - 1) / kCGroup;
     if (nb == 0) return hipSuccess;
     const uint32_t *off = hist + ng * kRadixBins;
-    hipLaunchKernelGGL(k_col_scatter, dim3((unsigned)nb), dim3(kCG), 0, s, perm, rect_sorted,
-                       rc_sorted, d_n, hist, ng, off, digit_total, pack_shift, out, cap, list_n);
+    const dim3 grid(xcd_run_grid(nb, kXcdColChunk));
+    hipLaunchKernelGGL(k_col_scatter, grid, dim3(kCG), 0, s, perm, rect_sorted, rc_sorted, d_n,
+                       hist, ng, off, digit_total, pack_shift, out, cap, list_n);
     return hipGetLastError();
 }

@@ -350,7 +350,8 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
         if (D <= (uint32_t)shift) return;
         n = ctl[0];
     }
-    const int64_t base = (int64_t)blockIdx.x * kDT;
+    const uint32_t tile = xcd_run_block(blockIdx.x, gridDim.x, kXcdSortChunk);
+    const int64_t base = (int64_t)tile * kDT;
     if (base >= n) return;
     const int nbits = pass_bits(shift);
     // msd: the pass sorted the top digit; it is the whole sort only when D <= 12 (shift 0)
@@ -382,7 +383,7 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
         uint4 c0 = make_uint4(0u, 0u, 0u, 0u), c1 = c0, h0 = c0, h1 = c0;
         if (d0 < nbins) {
             const uint4 *t4 = reinterpret_cast<const uint4 *>(digit_total + d0);
-            const uint4 *h4 = reinterpret_cast<const uint4 *>(hist + (int64_t)blockIdx.x * kDBins + d0);
+            const uint4 *h4 = reinterpret_cast<const uint4 *>(hist + (int64_t)tile * kDBins + d0);
             c0 = t4[0];
             c1 = t4[1];
             h0 = h4[0];
@@ -928,6 +929,7 @@ static hipError_t ds_passes(const uint32_t *keys, const uint32_t *ids_in, const 
                             uint32_t *hist, uint32_t *digit_total, uint32_t *ctl, int pass_begin,
                             int pass_end, unsigned long long *host_D, uint32_t tag, hipStream_t s) {
     const unsigned nt = (unsigned)((n + kDT - 1) / kDT);
+    const dim3 down_grid(xcd_run_grid(nt, kXcdSortChunk));  // (the downsweep's XCD runs)
     const void *in[kDPasses] = {keys, pairs_a, pairs_b};
     uint2 *out[kDPasses] = {pairs_a, pairs_b, nullptr};
     for (int p = pass_begin; p < pass_end; ++p) {
@@ -937,15 +939,17 @@ static hipError_t ds_passes(const uint32_t *keys, const uint32_t *ids_in, const 
                                ctl, shift, hist, d_n, 0);
             hipLaunchKernelGGL(k_ds_scan<true>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist,
                                n, ctl, shift, digit_total, d_n, host_D, tag, 0);
-            hipLaunchKernelGGL(k_ds_downsweep<true>, dim3(nt), dim3(kDThreads), 0, s, in[p], out[p],
-                               perm, n, drop, ctl, shift, hist, digit_total, ids_in, d_n, 0);
+            hipLaunchKernelGGL(k_ds_downsweep<true>, down_grid, dim3(kDThreads), 0, s, in[p],
+                               out[p], perm, n, drop, ctl, shift, hist, digit_total, ids_in, d_n,
+                               0);
         } else {
             hipLaunchKernelGGL(k_ds_upsweep<false>, dim3(nt), dim3(kDThreads), 0, s, in[p], n, 0,
                                ctl, shift, hist, nullptr, 0);
             hipLaunchKernelGGL(k_ds_scan<false>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist,
                                n, ctl, shift, digit_total, nullptr, nullptr, 0u, 0);
-            hipLaunchKernelGGL(k_ds_downsweep<false>, dim3(nt), dim3(kDThreads), 0, s, in[p],
-                               out[p], perm, n, 0, ctl, shift, hist, digit_total, nullptr, nullptr, 0);
+            hipLaunchKernelGGL(k_ds_downsweep<false>, down_grid, dim3(kDThreads), 0, s, in[p],
+                               out[p], perm, n, 0, ctl, shift, hist, digit_total, nullptr, nullptr,
+                               0);
         }
     }
     return hipGetLastError();
@@ -976,8 +980,9 @@ static void msd_launch(const uint32_t *keys, const uint32_t *ids_in, const uint3
                        hist, d_n, 1);
     hipLaunchKernelGGL(k_ds_scan<true>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist, n, ctl,
                        0, digit_total, d_n, host_D, tag, 1);
-    hipLaunchKernelGGL(k_ds_downsweep<true>, dim3(nt), dim3(kDThreads), 0, s, keys, pairs_a, perm,
-                       n, drop, ctl, 0, hist, digit_total, ids_in, d_n, 1);
+    hipLaunchKernelGGL(k_ds_downsweep<true>, dim3(xcd_run_grid(nt, kXcdSortChunk)),
+                       dim3(kDThreads), 0, s, keys, pairs_a, perm, n, drop, ctl, 0, hist,
+                       digit_total, ids_in, d_n, 1);
     if (wide)
         hipLaunchKernelGGL(k_ds_local<kLSlotsWide>, dim3(kDBins / kLGroup), dim3(kDThreads), 0, s,
                            pairs_a, pairs_b, perm, ctl, digit_total, host_crowd, tag);

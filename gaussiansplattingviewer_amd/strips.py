@@ -161,6 +161,11 @@ class StripGather:
         } for _ in range(depth)]
         self.next_slot = 0
         self.pending = []  # slots in flight, oldest first
+        # gloo moves device tensors from its own host threads, outside stream order: a submit
+        # then waits for the current stream (the render of the strip, earlier reads of the
+        # frame slot it receives into) before posting the transfers
+        dev = self.slots[0]["send"].device
+        self.host_transport = dev.type == "cuda" and dist.get_backend(group) != "nccl"
 
     def next_buffer(self, rows: int) -> torch.Tensor:
         """The (3, rows, W) render target of the next `submit`, ordered on the current stream
@@ -200,6 +205,8 @@ class StripGather:
             for c in range(3):
                 if rows:
                     ops.append(dist.P2POp(dist.isend, buf[c], 0, group=self.group))
+        if ops and self.host_transport:
+            torch.cuda.current_stream(buf.device).synchronize()
         slot["reqs"] = dist.batch_isend_irecv(ops) if ops else []
         slot["layout"] = list(layout)
         self.pending.append(slot)
