@@ -453,7 +453,7 @@ __global__ __launch_bounds__(kCG) void k_col_count(const uint32_t *__restrict__ 
     __shared__ uint32_t s_diff[kCGroup][kRadixBins + 1];
     __shared__ uint32_t s_tmp[4];
     const int tid = threadIdx.x;
-    const uint32_t gb = xcd_run_block(blockIdx.x, gridDim.x, kXcdColChunk);  // the group
+    const uint32_t gb = xcd_run_block(blockIdx.x);  // the group
     const int64_t n = *d_n;
     const int64_t base = (int64_t)gb * (kCG * kCGroup);
     if (base >= n) return;  // whole group (k_rs_scan reads groups [0, ceil(n / 1024)) only)
@@ -523,7 +523,7 @@ __global__ __launch_bounds__(kCG) void k_col_scatter(const uint32_t *__restrict_
         RadixTileSmem<kCW, kCIt / 2> small;
     } sm;
     const int tid = threadIdx.x;
-    const uint32_t blk = xcd_run_block(blockIdx.x, gridDim.x, kXcdColChunk);
+    const uint32_t blk = xcd_run_block(blockIdx.x);
     // global start of column d for this block's segments: all earlier columns (then earlier
     // blocks, below); the total is the list length
     uint32_t tot;
@@ -932,7 +932,7 @@ hipError_t gsr_launch_col_pairs_count(const uint32_t *perm, const uint2 *strip_r
     const int64_t nb = (n_max + kCG - 1) / kCG, ng = (nb + kCGroup - 1) / kCGroup;
     if (nb == 0) return hipSuccess;
     uint32_t *off = hist + ng * kRadixBins;
-    const dim3 grid(xcd_run_grid(ng, kXcdColChunk));
+    const dim3 grid(xcd_run_grid(ng));
     hipLaunchKernelGGL(k_col_count, grid, dim3(kCG), 0, s, perm, strip_rect, strip_rc, d_n,
                        rect_sorted, rc_sorted, hist, ng, off);
     return gsr_launch_digit_scan_n(hist, ng, digit_total, d_n, kCG * kCGroup, s);
@@ -946,7 +946,7 @@ hipError_t gsr_launch_col_pairs_scatter(const uint32_t *perm, const uint2 *rect_
     const int64_t nb = (n_max + kCG - 1) / kCG, ng = (nb + kCGroup - 1) / kCGroup;
     if (nb == 0) return hipSuccess;
     const uint32_t *off = hist + ng * kRadixBins;
-    const dim3 grid(xcd_run_grid(nb, kXcdColChunk));
+    const dim3 grid(xcd_run_grid(nb));
     hipLaunchKernelGGL(k_col_scatter, grid, dim3(kCG), 0, s, perm, rect_sorted, rc_sorted, d_n,
                        hist, ng, off, digit_total, pack_shift, out, cap, list_n);
     return hipGetLastError();

@@ -350,7 +350,7 @@ __global__ __launch_bounds__(kDThreads) void k_ds_downsweep(
         if (D <= (uint32_t)shift) return;
         n = ctl[0];
     }
-    const uint32_t tile = xcd_run_block(blockIdx.x, gridDim.x, kXcdSortChunk);
+    const uint32_t tile = xcd_run_block(blockIdx.x);
     const int64_t base = (int64_t)tile * kDT;
     if (base >= n) return;
     const int nbits = pass_bits(shift);
@@ -929,7 +929,7 @@ static hipError_t ds_passes(const uint32_t *keys, const uint32_t *ids_in, const 
                             uint32_t *hist, uint32_t *digit_total, uint32_t *ctl, int pass_begin,
                             int pass_end, unsigned long long *host_D, uint32_t tag, hipStream_t s) {
     const unsigned nt = (unsigned)((n + kDT - 1) / kDT);
-    const dim3 down_grid(xcd_run_grid(nt, kXcdSortChunk));  // (the downsweep's XCD runs)
+    const dim3 down_grid(xcd_run_grid(nt));  // (the downsweep's XCD runs)
     const void *in[kDPasses] = {keys, pairs_a, pairs_b};
     uint2 *out[kDPasses] = {pairs_a, pairs_b, nullptr};
     for (int p = pass_begin; p < pass_end; ++p) {
@@ -980,7 +980,7 @@ static void msd_launch(const uint32_t *keys, const uint32_t *ids_in, const uint3
                        hist, d_n, 1);
     hipLaunchKernelGGL(k_ds_scan<true>, dim3(kDBins / kScanDigits), dim3(256), 0, s, hist, n, ctl,
                        0, digit_total, d_n, host_D, tag, 1);
-    hipLaunchKernelGGL(k_ds_downsweep<true>, dim3(xcd_run_grid(nt, kXcdSortChunk)),
+    hipLaunchKernelGGL(k_ds_downsweep<true>, dim3(xcd_run_grid(nt)),
                        dim3(kDThreads), 0, s, keys, pairs_a, perm, n, drop, ctl, 0, hist,
                        digit_total, ids_in, d_n, 1);
     if (wide)

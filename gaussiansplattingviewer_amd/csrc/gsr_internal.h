@@ -242,26 +242,22 @@ __device__ __forceinline__ uint32_t block256_exclusive_scan(uint32_t v, uint32_t
 }
 
 // --- XCD-aware block order for the scattering passes ---------------------------------------
-// The hardware deals workgroup b to XCD b % 8.  Logical block order: chunks of `chunk`
-// consecutive logical blocks go to one XCD, the chunks round-robin over the XCDs (chunk 0: one
-// contiguous run per XCD), so the partial lines that neighbouring blocks write into one digit's
-// run meet in one L2 and leave it merged.  G = gridDim.x, a multiple of 8 * chunk
-// (xcd_run_grid).  Speed only: every logical block does the same work.
-// The column pass (k_col_count, k_col_scatter) works on depth-ordered blocks whose work falls
-// with depth (near splats are large), so whole runs per XCD would unbalance the XCDs: chunks
-// of 16 blocks.  The radix passes' tiles are uniform: one run per XCD.  (C3 +2.5 % in flight,
-// serial -1.5 %, C4 full frame +7 %, profiles/r06k_ab_xcd_runs.txt.)
-constexpr int kXcdColChunk = 16;
-constexpr int kXcdSortChunk = 0;
-__device__ __forceinline__ uint32_t xcd_run_block(uint32_t b, uint32_t G, int chunk) {
+// The hardware deals workgroup b to XCD b % 8.  Here chunks of kXcdChunk consecutive logical
+// blocks go to one XCD, the chunks round-robin over the XCDs, so the partial lines that
+// neighbouring blocks write into one digit's run meet in one L2 and leave it merged, while the
+// XCDs stay balanced (the column pass's depth-ordered blocks shrink with depth) and the live
+// blocks of a grid sized for capacity (a device-side count) still come first on every XCD.
+// The grid is a multiple of 8 kXcdChunk blocks (xcd_run_grid); speed only, every logical block
+// does the same work.  One contiguous run per XCD lost on both counts
+// (profiles/r06k_ab_xcd_runs.txt, r06n_ab_xcd_sort_chunk.txt); chunks of 16 gain C3 +2 %, the
+// C4 full frame +7 %.
+constexpr uint32_t kXcdChunk = 16;
+__device__ __forceinline__ uint32_t xcd_run_block(uint32_t b) {
     const uint32_t x = b & 7u, l = b >> 3;
-    if (chunk < 0) return b;
-    if (chunk == 0) return x * (G >> 3) + l;
-    const uint32_t c = (uint32_t)chunk;
-    return ((l / c) * 8u + x) * c + l % c;
+    return ((l / kXcdChunk) * 8u + x) * kXcdChunk + l % kXcdChunk;
 }
-inline uint32_t xcd_run_grid(int64_t nb, int chunk) {
-    const int64_t m = chunk < 0 ? 1 : chunk == 0 ? 8 : 8 * (int64_t)chunk;
+inline uint32_t xcd_run_grid(int64_t nb) {
+    const int64_t m = 8 * (int64_t)kXcdChunk;
     return (uint32_t)((nb + m - 1) / m * m);
 }
 

@@ -62,7 +62,7 @@ __global__ __launch_bounds__(kW * 64) void k_rs_upsweep(const uint32_t *__restri
     static_assert(kTiles == 1 || kTiles == 4, "one tile or a 16-B word of four");
     __shared__ uint32_t s_hist[kW][kRadix];
     const int tid = threadIdx.x, w = tid >> 6;
-    const int64_t tile0 = (int64_t)xcd_run_block(blockIdx.x, gridDim.x, kXcdSortChunk) * kTiles;
+    const int64_t tile0 = (int64_t)xcd_run_block(blockIdx.x) * kTiles;
     if (tile0 * kT >= n) return;  // whole block (the scan reads columns [0, ceil(n / kT)) only)
     uint32_t cnt[kTiles];
     for (int t = 0; t < kTiles; ++t) {
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(kW * 64) void k_rs_downsweep(
     __shared__ uint32_t s_vals[kVals ? kT : 1];
     __shared__ RadixTileSmem<kW, kIt> sm;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t tile = xcd_run_block(blockIdx.x, gridDim.x, kXcdSortChunk);
+    const uint32_t tile = xcd_run_block(blockIdx.x);
     const int64_t base = (int64_t)tile * kT;
     if (base >= n) return;  // whole block
     uint32_t k[kIt], v[kIt];
@@ -233,16 +233,16 @@ static void rts_pass(const uint32_t *k, const uint32_t *v, uint32_t *ko, uint32_
     const uint32_t mask = (1u << nbits) - 1u;
     if (nb >= kQuadTiles)
         hipLaunchKernelGGL((k_rs_upsweep<kSW, kSIt, 4>),
-                           dim3(xcd_run_grid((nb + 3) / 4, kXcdSortChunk)), dim3(kSW * 64), 0, s,
+                           dim3(xcd_run_grid((nb + 3) / 4)), dim3(kSW * 64), 0, s,
                            k, n, shift, mask, hist, stride, d_n);
     else
-        hipLaunchKernelGGL((k_rs_upsweep<kSW, kSIt, 1>), dim3(xcd_run_grid(nb, kXcdSortChunk)),
+        hipLaunchKernelGGL((k_rs_upsweep<kSW, kSIt, 1>), dim3(xcd_run_grid(nb)),
                            dim3(kSW * 64), 0, s, k, n, shift, mask, hist, stride, d_n);
     // (with d_n, an over-capacity count scans stale counts, in bounds; the downsweep then
     // sorts nothing)
     hipLaunchKernelGGL(k_rs_scan, dim3(kRadix), dim3(kBlock), 0, s, hist, stride, digit_total,
                        RsCount{nb, d_n}, kST);
-    const dim3 down_grid(xcd_run_grid(nb, kXcdSortChunk));
+    const dim3 down_grid(xcd_run_grid(nb));
     if (v)
         hipLaunchKernelGGL((k_rs_downsweep<kSW, kSIt, true>), down_grid, dim3(kSW * 64), 0, s, k,
                            v, ko, vo, n, shift, nbits, hist, digit_total, stride, d_n);
