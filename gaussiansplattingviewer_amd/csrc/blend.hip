@@ -2,7 +2,9 @@
 //
 // Replaces upstream diff-gaussian-rasterization forward.cu renderCUDA (GLSL twin of the
 // per-pixel alpha: shaders/gau_frag.glsl:21-27).  k_blend_q: one wave per (16x16 tile, 8x8
-// quadrant), one pixel per lane, 64-thread blocks, no block barriers.  Each wave streams its
+// quadrant), one pixel per lane, a tile's four quadrant waves in one 256-thread block that never
+// synchronises (each wave is independent; one block per tile instead of one per quadrant:
+// blend -2 %, C3 +2 % in flight, profiles/r06p_ab_blend_tile_blocks.txt).  Each wave streams its
 // tile's depth-sorted list 64 splats at a time, culls them against its own quadrant (the
 // splat's conservative alpha >= 1/255 ellipse from preprocess.hip cull_data: bounding box,
 // then the exact ellipse-vs-box minimum with a rounding bound), compacts the survivors into
@@ -73,19 +75,19 @@ __device__ __forceinline__ bool may_touch(float x, float y, float A, float B, fl
     return !(lb > twoL);
 }
 
-// Block -> work item, XCD-aware: the hardware deals block b to XCD b % 8 (speed only, never
-// correctness); groups of kXcdGroup consecutive work items (four row-adjacent tiles' quadrants)
-// go round-robin over the XCDs, so each group shares one L2 while the image's heavy and light
-// regions are spread evenly over the 8 XCDs.  With `order` (k_blend_order) the groups are
+// Block -> tile, XCD-aware: the hardware deals block b to XCD b % 8 (speed only, never
+// correctness); groups of kGroupTiles consecutive tiles (four row-adjacent tiles, 16 quadrant
+// waves) go round-robin over the XCDs, so each group shares one L2 while the image's heavy and
+// light regions are spread evenly over the 8 XCDs.  With `order` (k_blend_order) the groups are
 // dealt heaviest first: every wave of the last round is then a short one, and the kernel's
 // tail -- the last waves finishing on an emptying chip -- shrinks.
-constexpr uint32_t kXcdGroup = 16;
-__device__ __forceinline__ uint32_t xcd_work(uint32_t b, const uint32_t *order,
+constexpr uint32_t kGroupTiles = 4;
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, const uint32_t *order,
                                              uint32_t n_groups) {
     const uint32_t x = b & 7u, l = b >> 3;
-    uint32_t g = (l / kXcdGroup) * 8u + x;
+    uint32_t g = (l / kGroupTiles) * 8u + x;
     if (order && g < n_groups) g = order[g];
-    return g * kXcdGroup + l % kXcdGroup;
+    return g * kGroupTiles + l % kGroupTiles;
 }
 
 // Counting sort of the tile groups by a log-scale pair count, descending (one block; order
@@ -94,9 +96,9 @@ __device__ __forceinline__ uint32_t xcd_work(uint32_t b, const uint32_t *order,
 constexpr int kOrderBuckets = 1024;
 __device__ __forceinline__ uint32_t order_key(const uint2 *ranges, uint32_t g, uint32_t n_tiles) {
     uint32_t n = 0;
-    const uint32_t t0 = g * (kXcdGroup / 4u);
+    const uint32_t t0 = g * kGroupTiles;
 #pragma unroll
-    for (uint32_t i = 0; i < kXcdGroup / 4u; ++i)
+    for (uint32_t i = 0; i < kGroupTiles; ++i)
         if (t0 + i < n_tiles) {
             const uint2 r = ranges[t0 + i];
             n += r.y - r.x;
@@ -157,7 +159,7 @@ struct StagedSplat {
     float4 e;
 };
 
-// Blocks are mapped XCD-aware (xcd_work).  Only the next chunk's point-list ids are
+// Blocks are mapped XCD-aware (xcd_tile).  Only the next chunk's point-list ids are
 // prefetched (no record prefetch): the kernel fits 64 VGPRs and 8 waves per SIMD, and the
 // record gathers' latency is left to the other waves (a record prefetch spilled at 8 waves
 // and lost at fewer).  A block per tile with shared staging lost to independent
@@ -167,16 +169,16 @@ struct StagedSplat {
 // kContrib: track the last contributor (the n_contrib output); off (no n_contrib requested),
 // the composite step loses one v_cndmask.
 template <bool kFast, bool kContrib>
-__global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_t n_work) {
-    __shared__ StagedSplat s_spl[64];
+__global__ __launch_bounds__(256, 8) void k_blend_q(const GsrBlendArgs a, uint32_t n_tiles) {
+    __shared__ StagedSplat s_spl_q[4][64];  // per quadrant wave
     constexpr bool kPair = kFast && !kContrib;  // paired colour / bound words (see staging)
 
-    const uint32_t b = blockIdx.x;
-    const uint32_t work = xcd_work(b, a.order, (n_work + kXcdGroup - 1) / kXcdGroup);
-    if (work >= n_work) return;
+    const uint32_t tile = xcd_tile(blockIdx.x, a.order, (n_tiles + kGroupTiles - 1) / kGroupTiles);
+    if (tile >= n_tiles) return;
     if (a.list_n && *a.list_n > a.list_cap) return;  // not binned (frame graphs: re-rendered)
-    const int lane = threadIdx.x;
-    const uint32_t tile = work >> 2, quad = work & 3u;
+    const uint32_t quad = threadIdx.x >> 6;  // this wave's quadrant
+    const int lane = threadIdx.x & 63;
+    StagedSplat *const s_spl = s_spl_q[quad];
     const uint32_t tx = tile % a.grid_x, ty_local = tile / a.grid_x, ty = a.row_begin + ty_local;
     const int qx0 = (int)tx * GSR_TILE_X + (int)(quad & 1u) * 8;
     const int qy0 = (int)ty * GSR_TILE_Y + (int)(quad >> 1) * 8;
@@ -359,16 +361,17 @@ __global__ __launch_bounds__(64, 8) void k_blend_q(const GsrBlendArgs a, uint32_
     }
 }
 
-// Grid of whole XCD groups: n_work items, kXcdGroup per XCD round; blocks past n_work exit.
-inline uint32_t xcd_grid(uint32_t n_work) {
-    const uint32_t g = kXcdGroup * 8u;
-    return (n_work + g - 1) / g * g;
+// Grid of whole XCD groups: one block per tile, kGroupTiles per XCD round; blocks past the
+// last tile exit.
+inline uint32_t xcd_grid(uint32_t n_tiles) {
+    const uint32_t g = kGroupTiles * 8u;
+    return (n_tiles + g - 1) / g * g;
 }
 
 }  // namespace
 
 uint32_t gsr_blend_order_groups(uint32_t n_tiles) {
-    return (4u * n_tiles + kXcdGroup - 1) / kXcdGroup;
+    return (n_tiles + kGroupTiles - 1) / kGroupTiles;
 }
 
 hipError_t gsr_launch_blend_order(const uint2 *ranges, uint32_t n_tiles, uint32_t *order,
@@ -381,13 +384,13 @@ hipError_t gsr_launch_blend_order(const uint2 *ranges, uint32_t n_tiles, uint32_
 
 hipError_t gsr_launch_blend(const GsrBlendArgs &a, hipStream_t s) {
     if (a.rows_tiles == 0 || a.grid_x == 0) return hipSuccess;
-    const uint32_t n_work = 4u * a.grid_x * a.rows_tiles;
-    const dim3 grid(xcd_grid(n_work));
+    const uint32_t n_tiles = a.grid_x * a.rows_tiles;
+    const dim3 grid(xcd_grid(n_tiles));
     if (a.fast && !a.n_contrib)
-        hipLaunchKernelGGL((k_blend_q<true, false>), grid, dim3(64), 0, s, a, n_work);
+        hipLaunchKernelGGL((k_blend_q<true, false>), grid, dim3(256), 0, s, a, n_tiles);
     else if (a.fast)
-        hipLaunchKernelGGL((k_blend_q<true, true>), grid, dim3(64), 0, s, a, n_work);
+        hipLaunchKernelGGL((k_blend_q<true, true>), grid, dim3(256), 0, s, a, n_tiles);
     else
-        hipLaunchKernelGGL((k_blend_q<false, true>), grid, dim3(64), 0, s, a, n_work);
+        hipLaunchKernelGGL((k_blend_q<false, true>), grid, dim3(256), 0, s, a, n_tiles);
     return hipGetLastError();
 }

@@ -25,15 +25,16 @@ def make():
     src = open(os.path.join(REPO, "gaussiansplattingviewer_amd/csrc/blend.hip")).read()
     patches = [
         ("namespace {\n", "namespace {\n__device__ uint4 g_trace[1 << 16];\n", 1),
-        ("    if (work >= n_work) return;\n",
-         "    if (work >= n_work) return;\n"
+        ("    StagedSplat *const s_spl = s_spl_q[quad];\n",
+         "    StagedSplat *const s_spl = s_spl_q[quad];\n"
+         "    const uint32_t work = tile * 4u + quad;  // (trace slot: one per quadrant wave)\n"
          "    const uint32_t t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();\n"
          "    uint32_t n_chunks = 0, n_comp = 0;\n", 1),
         ("    for (uint32_t start = range.x; start < range.y; start += 64) {\n",
          "    for (uint32_t start = range.x; start < range.y; start += 64) {\n        ++n_chunks;\n", 1),
         ("            ++count;\n        }\n", "            ++count;\n        }\n        n_comp += count;\n", 1),
         ("    if (inside) {\n        const int row = py - a.y0;",
-         "    if (threadIdx.x == 0 && work < (1u << 16)) {\n"
+         "    if (lane == 0 && work < (1u << 16)) {\n"
          "        const uint32_t t_end = (uint32_t)__builtin_amdgcn_s_memrealtime();\n"
          "        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);\n"
          "        const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);\n"
