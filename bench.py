@@ -3,11 +3,11 @@
 Headline workload (BASELINE.json configs[2] = SURVEY.md §8(d) C3): 1M synthetic Gaussians,
 SH degree 3, 1920x1080, static camera, inputs resident in HBM.  One step = one full frame:
 preprocess (EWA + SH) -> device radix depth sort -> binning -> tile sort -> ranges -> blend,
-including the per-frame K readback the algorithm needs.  Two frames are in flight by
-default (--inflight, `FramePipeline`: frame i on stream / context slot i % 2, so the next
-frame's latency-bound preprocess and sort overlap this frame's VALU-bound blend; every frame
-is still rendered in full and bit-identically); `serial_ms_per_frame` reports one frame at a
-time.  With --gpus N (one process per GPU,
+including the per-frame K readback the algorithm needs.  Four frames are in flight by
+default (--inflight, `FramePipeline`: frame i on stream / context slot i % 4, one stream per
+frame, so the next frames' latency-bound preprocess, sort and binning overlap this frame's
+VALU-bound blend; every frame is still rendered in full and bit-identically);
+`serial_ms_per_frame` reports one frame at a time.  With --gpus N (one process per GPU,
 launched by torch.distributed.run) the frame's 16-px tile rows are split into N strips, every
 rank renders its strip and rank 0 gathers the frame over RCCL (strong scaling: the frame is
 fixed, N grows).  The untimed diagnostic passes (serial frame time, stage breakdown, in-flight
@@ -31,9 +31,16 @@ import platform
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
+# A strip rank (N > 1) runs RCCL's streams (torch's NCCL stream, RCCL's own) beside its frame
+# streams; with HIP's default of 4 hardware queues per process a frame stream would share a
+# queue with them (DESIGN.md §5 "Queue budget").  Ranks take 8, set before HIP initialises
+# (8 queues measured even at N = 1: profiles/r05z3_ab_hw_queues.txt, r05k_ab_depth_queues.txt).
+if int(os.environ.get("WORLD_SIZE", "1")) > 1 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
@@ -646,8 +653,12 @@ def main():
                               "used by the in-flight pass" if world == 1 else
                               "RCCL's communicators (warm-up all-reduce + gather), then the "
                               "FramePipeline streams in slot order"),
-                    "note": "HIP fixes a stream's hardware queue (GPU_MAX_HW_QUEUES = 4) when "
-                            "the stream is first used; the plan stays within 4 streams"},
+                    "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                    "note": ("HIP fixes a stream's hardware queue when the stream is first used; "
+                             "the plan stays within the process's hw_queues" if world == 1 else
+                             "HIP fixes a stream's hardware queue when the stream is first used; "
+                             "a rank takes 8 queues so that RCCL's streams do not share the "
+                             "frame streams' queues")},
         "timed_after": ("194 serial (64 untimed, 100 for the serial rate, 30 with stage events) "
                         "then 64 in-flight (blend events) untimed diagnostic frames, then the W "
                         "warmup frames" if world == 1 else

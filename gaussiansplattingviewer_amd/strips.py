@@ -132,8 +132,9 @@ def rank_stream_plan(inflight: int, second_stream: bool) -> list[str]:
     """The HIP streams one rank's frame loop uses (bench.py): the caller's stream
     and inflight - 1 FramePipeline streams, plus each in-flight context's second stream when on.
     StripBalancer and StripGather create none (RCCL's collectives run on RCCL's own streams,
-    created with the communicator before these).  With GPU_MAX_HW_QUEUES = 4 the plan must stay
-    within 4 for every frame stream to have a hardware queue of its own."""
+    created with the communicator before these).  The plan stays within 4 streams (HIP's default
+    GPU_MAX_HW_QUEUES); bench.py gives a rank of N > 1 eight queues, so RCCL's streams get
+    queues of their own beside it."""
     plan = ["caller"] + [f"frame{i}" for i in range(1, inflight)]
     if second_stream:
         plan += [f"second{i}" for i in range(inflight)]
