@@ -542,9 +542,15 @@ int launch_depth_sort(gsr_context *ctx, const Frame &f, int p0, int p1) {
 // colour waves per SIMD (gsr_launch_color): 2 on a full frame, so the colour leaves the CUs
 // to the binning chain it overlaps (C3 two frames in flight 3,890-3,918 -> 3,947-3,954
 // frames/s, serial 0.317 -> 0.308 ms; C4 serial 2.09 -> 2.06 ms); 3 on a compacted strip
-// (C4 1/8 strip 0.481 -> 0.468 ms).  profiles/r04n_ab_color_waves.txt, DESIGN.md decision 7
-constexpr int kColorWavesFull = 2;
-int color_waves_of(const Frame &f) { return f.color_ids ? 3 : kColorWavesFull; }
+// (C4 1/8 strip 0.481 -> 0.468 ms).  profiles/r04n_ab_color_waves.txt, DESIGN.md decision 7.
+// 4 on a strip that is not compacted: its waves scan every Gaussian and only ~1 lane in 8 has
+// a colour to compute, so more of them hide the row loads' latency (C3 strips +2-3 %, colour
+// 49 -> 44 us, profiles/r06x_ab_strip_colour_cap.txt).
+constexpr int kColorWavesFull = 2, kColorWavesCompacted = 3, kColorWavesStrip = 4;
+int color_waves_of(const Frame &f) {
+    if (f.color_ids) return kColorWavesCompacted;
+    return f.rows_tiles < f.gy ? kColorWavesStrip : kColorWavesFull;
+}
 
 // ---- the second stream: K, the tile ranges (column pairs), the colour -----------------------
 // The second stream's kernels on stream `as` (a frame graph records them on its capture
