@@ -460,9 +460,14 @@ def main():
         opt(_lib.GSR_OPT_DEPTH_SORT,
             {"auto": -1, "lsd": 0, "compact": 1, "msd": 2, "compact-msd": 3}[args.depth_sort])
     # frame graphs: the pipeline's choice (strip frames in flight) unless --graphs; the serial
-    # passes render as a caller without the pipeline does (direct launches)
+    # passes render as a caller without the pipeline does (direct launches).  Full frames of
+    # small scenes are host-bound (~17 launches per frame): recorded graphs there (C1 +16-28 %,
+    # C2 +3-4 %, profiles/r06zb_ab_small_frame_graphs.txt); from 512k Gaussians direct launches
+    # (a graph adds ~20 us to a frame's latency, which the 20-frame window pays: C3 -2.6 %,
+    # r06h_ab_graphs_one_stream.txt)
+    small_frame_graphs = not strip and args.inflight >= 2 and scene.P < (512 << 10)
     graphs_inflight = (args.graphs if args.graphs is not None else
-                       1 if strip_graphs else 2 if small_strip else 0)
+                       1 if (strip_graphs or small_frame_graphs) else 2 if small_strip else 0)
     graphs_serial = args.graphs if args.graphs is not None else 0
     names = _lib.stage_names()
     buf = (ctypes.c_float * len(names))()
