@@ -678,10 +678,11 @@ def main():
                          **{f"slot{c}": _lib.frame_graph_stats(local, c)
                             for c in range(args.inflight)},
                          "note": "GSR_OPT_FRAME_GRAPHS of the in-flight frames (0 direct "
-                                 "launches: full frames; 2 deferred-K chains on one stream: "
-                                 "strip frames below 4M Gaussians; 1 recorded graphs: larger "
-                                 "strip frames, two in flight) and of the serial pass (direct "
-                                 "launches, as a caller without the pipeline)"},
+                                 "launches: full frames from 512k Gaussians; 1 recorded graphs: "
+                                 "full frames of smaller scenes, and strip frames from 4M "
+                                 "Gaussians, two in flight; 2 deferred-K chains on one stream: "
+                                 "strip frames below 4M Gaussians) and of the serial pass "
+                                 "(direct launches, as a caller without the pipeline)"},
         "serial_ms_per_frame": round(serial_ms, 4),
         "serial_note": "one frame in flight at a time (no FramePipeline overlap), this rank",
         "roofline": roofline,
