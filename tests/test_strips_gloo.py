@@ -14,6 +14,8 @@ import torch.multiprocessing as mp
 
 from gaussiansplattingviewer_amd.strips import gather_strips, render_strips, strip_pixel_rows, strip_rows
 
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 
 def _free_port():
     s = socket.socket()
@@ -234,3 +236,23 @@ def test_strip_rank_stream_budget(tmp_path, world):
     assert len(rank_stream_plan(2, True)) == 4
     assert len(rank_stream_plan(4, False)) == 4
     assert len(rank_stream_plan(3, True)) > 4  # (the combination the bench avoids)
+
+
+@pytest.mark.parametrize("world,preset,expect", [("2", None, "8"), ("8", "4", "8"), ("1", None, None),
+                                                 ("2", "16", "16")])
+def test_bench_rank_hw_queues(world, preset, expect):
+    """bench.py gives a rank of N > 1 eight hardware queues before HIP initialises (RCCL's
+    streams beside the four frame streams, DESIGN.md §5 "Queue budget"), leaves N = 1 at HIP's
+    default and never lowers a larger setting."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    env["WORLD_SIZE"] = world
+    if preset is not None:
+        env["GPU_MAX_HW_QUEUES"] = preset
+    code = ("import os, sys; sys.argv = ['bench.py']; import bench; "
+            "print(os.environ.get('GPU_MAX_HW_QUEUES', 'unset'))")
+    out = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.strip().splitlines()[-1] == (expect or "unset")
